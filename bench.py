@@ -1,0 +1,213 @@
+"""Benchmark: the frame-differencing hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): one synthetic 1920x1080 camera feed per
+GPU (seed = rank), the full per-frame worker of frame_differencing.py:91-133 —
+gray, 5x5 blur, absdiff/threshold, contour-area filter, 7x7 dilate,
+accumulation, red overlay, static-block DCT quantisation, YCrCb round trip —
+with the GUI's default kwargs (windows.py:154). Frames are device-resident: a
+ring of 64 distinct frames (398 MB, beyond the 256 MB Infinity Cache) played
+ping-pong (0..63..1) so every consecutive pair is real motion; overlay and
+compressed outputs go to 126-slot device rings. A step = one 126-frame pass,
+captured once as a hipGraph and replayed.
+
+Feeds shard one per GPU with no data-path collective ("scaling": "weak");
+RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
+
+Extra JSON fields: ``roofline`` for the dominant kernel (k_back: hipEvent time
+per launch on the feed's stream, in a second pass of the same steps) and
+``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
+feed; rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpixels/s (frames/s × H×W) 1080p frame-diff path @1/2/4/8 GPU; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BACK_BYTES_PER_PX = 11         # k_back algorithmic: read BGR 3 + acc 1; write acc 1 + overlay 3 + compressed 3
+PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 read, new gray 1 written
+
+
+def pingpong(n: int):
+    return list(range(n)) + list(range(n - 2, 0, -1))
+
+
+def pmc_traffic(path: str, kernel_prefix: str):
+    """HBM bytes per launch of a kernel from a committed rocprofv3 PMC summary, or None."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel_prefix]
+        return float(k["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int):
+    import oracle  # checker / CPU baseline only
+    from dvc_amd.synthetic import SyntheticClip
+    oracle.build()
+    clip = SyntheticClip(width, height, seed=0)
+    o = oracle.OracleFD(width, height)
+    o.prime(clip.frame(0))
+    frames = [clip.frame(t) for t in range(1, max_frames + 1)]
+    n, t0 = 0, time.perf_counter()
+    for f in frames:
+        o.step(f)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"C oracle (oracle/dvc_oracle.c, -O3, 1 thread) on frames 1..{n} of the same "
+                      f"{width}x{height} synthetic feed (seed 0), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--ring", type=int, default=64)
+    ap.add_argument("--noisy", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="launch per frame instead of replaying a hipGraph")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import dvc_amd
+    from dvc_amd.synthetic import SyntheticClip
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, R = args.width, args.height, args.ring
+    clip = SyntheticClip(W, H, seed=rank, noisy=args.noisy)
+    ring = torch.empty((R, H, W, 3), dtype=torch.uint8, device=dev)
+    for i in range(R):
+        ring[i].copy_(torch.from_numpy(clip.frame(i)))
+    order = pingpong(R)
+    P = len(order)                 # frames per step (126 for R=64), even
+    ov = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
+    cp = torch.empty_like(ov)
+    torch.cuda.synchronize()
+
+    def make_worker(ktiming=False):
+        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming)
+        w.prime(ring[0])
+        return w
+
+    def run_steps(w, n, graph):
+        for _ in range(n):
+            if graph:
+                w.graph_launch()
+            else:
+                for j in range(P):
+                    w.step(ring[order[(j + 1) % P]], ov[j], cp[j])
+
+    w = make_worker()
+    graph = not args.eager
+    if graph:
+        w.graph_begin()
+        run_steps(w, 1, graph=False)
+        w.graph_end()
+    run_steps(w, args.warmup, graph)
+    w.sync()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    run_steps(w, args.steps, graph)
+    w.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    st = w.stats()
+    w.close()
+
+    # dominant kernel: hipEvent-timed k_back launches, same steps (eager: events need a plain stream)
+    wk = make_worker(ktiming=True)
+    run_steps(wk, 1, graph=False)
+    wk.ktime(reset=True)
+    run_steps(wk, max(1, min(args.steps, 10)), graph=False)
+    kms, kn = wk.ktime()
+    wk.close()
+
+    vec = torch.tensor([elapsed, st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = vec[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)   # RCCL: end-of-run aggregate stats only
+        vec[0] = tmax[0]
+    elapsed_max = float(vec[0])
+    frames_total = args.steps * P * world
+    value = frames_total * W * H / elapsed_max / 1e6
+
+    if rank == 0:
+        avg_ms = kms / max(kn, 1)
+        achieved = BACK_BYTES_PER_PX * W * H / (avg_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_back")
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": "fd_1080p_single_feed_per_gpu" if (W, H) == (1920, 1080) else f"fd_{W}x{H}",
+                       "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": 1,
+                       "ring_frames": R, "noisy": args.noisy, "launch": "hipgraph" if graph else "eager",
+                       "parallelism": f"feed-per-gpu x{world}",
+                       "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
+                       "pipeline_bytes_per_px": PIPE_BYTES_PER_PX,
+                       "pipeline_GBps_per_gpu": round(PIPE_BYTES_PER_PX * args.steps * P * W * H / elapsed_max / 1e9, 1)},
+            "roofline": {"bound": "hbm", "kernel": "k_back", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": BACK_BYTES_PER_PX * W * H,
+                         "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn},
+            "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
+                      "static_blocks": int(vec[4])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,12 @@
+"""Import shim: ``import dvc_amd`` loads the package directory
+``dynamic-video-compression-surveillance_amd/`` (not a valid identifier)."""
+import importlib.util as _ilu
+import os as _os
+import sys as _sys
+
+_PKG_DIR = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "dynamic-video-compression-surveillance_amd")
+_spec = _ilu.spec_from_file_location(__name__, _os.path.join(_PKG_DIR, "__init__.py"),
+                                     submodule_search_locations=[_PKG_DIR])
+_mod = _ilu.module_from_spec(_spec)
+_sys.modules[__name__] = _mod
+_spec.loader.exec_module(_mod)

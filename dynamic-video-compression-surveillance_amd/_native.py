@@ -1,0 +1,162 @@
+"""ctypes binding of ``libdvc_hip.so`` — the C-ABI declared in ``include/dvc.h``.
+
+The reference has no FFI: it calls ``cv2.*`` inside the per-frame loop of
+``frame_differencing.py:85-138``. This module is the thin layer that replaces
+those calls with one ``dvc_fd_step`` per frame. There is deliberately no CPU
+fallback: if the HIP library is missing or fails to load, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
+SOURCES = ["fd_kernels.hip", "fd_api.hip"]
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
+
+DVC_OK = 0
+DVC_FLAG_DEVICE_PTRS = 0x1
+DVC_FLAG_KTIMING = 0x2
+DVC_FLAG_KEEP_PLANES = 0x4
+
+PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
+
+# every symbol include/dvc.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "dvc_abi_version", "dvc_last_error", "dvc_device_count", "dvc_fd_create", "dvc_fd_prime",
+    "dvc_fd_step", "dvc_fd_sync", "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime",
+    "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter",
+    "dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch",
+]
+
+
+class DvcError(RuntimeError):
+    """A negative status from the C-ABI (message from dvc_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"dvc error {code}: {msg}")
+        self.code = code
+
+
+class FdParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("block", ctypes.c_int32),
+        ("ithresh", ctypes.c_int32),
+        ("min_area2", ctypes.c_int64),
+        ("ksize", ctypes.c_int32),
+        ("anchor", ctypes.c_int32),
+        ("alpha", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("gamma", ctypes.c_float),
+        ("quant", ctypes.c_float),
+        ("prime_ksize", ctypes.c_int32),
+        ("prime_sigma", ctypes.c_double),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class FdStats(ctypes.Structure):
+    _fields_ = [
+        ("frames", ctypes.c_uint64),
+        ("motion_px", ctypes.c_uint64),
+        ("components", ctypes.c_uint64),
+        ("static_blocks", ctypes.c_uint64),
+    ]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP library in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, "fd_kernels.h"), os.path.join(PKG_DIR, "..", "include", "dvc.h")]
+    if not force and os.path.exists(LIB_PATH):
+        newest = max(os.path.getmtime(d) for d in deps if os.path.exists(d))
+        if os.path.getmtime(LIB_PATH) >= newest:
+            return LIB_PATH
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", tmp, *srcs]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdvc_hip.so. Raises (never falls back) if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the HIP path has no CPU fallback)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (same
+    # SONAME). Loading torch first makes libdvc_hip.so bind to that instance, so
+    # torch tensors/streams and this library share devices and streams; loading
+    # /opt/rocm's copy first would leave torch without a usable GPU.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8p = ctypes.c_void_p, ctypes.c_void_p
+    L.dvc_abi_version.restype = ctypes.c_int
+    L.dvc_last_error.restype = ctypes.c_char_p
+    L.dvc_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.dvc_fd_create.argtypes = [ctypes.POINTER(FdParams), ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.dvc_fd_prime.argtypes = [vp, u8p, ctypes.c_size_t]
+    L.dvc_fd_step.argtypes = [vp, u8p, ctypes.c_size_t, u8p, u8p, u8p]
+    L.dvc_fd_sync.argtypes = [vp]
+    L.dvc_fd_get_stats.argtypes = [vp, ctypes.POINTER(FdStats)]
+    L.dvc_fd_read_plane.argtypes = [vp, ctypes.c_int, u8p]
+    L.dvc_fd_ktime.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.dvc_fd_destroy.argtypes = [vp]
+    L.dvc_fd_destroy.restype = None
+    L.dvc_gaussian_taps_q8.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint16)]
+    for name in ("dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch"):
+        getattr(L, name).argtypes = [vp]
+    L.dvc_contour_filter.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, u8p,
+                                     ctypes.POINTER(ctypes.c_uint64)]
+    for name in ("dvc_device_count", "dvc_fd_create", "dvc_fd_prime", "dvc_fd_step", "dvc_fd_sync",
+                 "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime", "dvc_gaussian_taps_q8",
+                 "dvc_contour_filter", "dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch"):
+        getattr(L, name).restype = ctypes.c_int
+    if L.dvc_abi_version() != 1:
+        raise ImportError("libdvc_hip.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != DVC_OK:
+        msg = lib().dvc_last_error()
+        raise DvcError(rc, msg.decode() if msg else "")
+
+
+def contour_filter(mask, min_area2: int, device: int = 0):
+    """fd:100-104 on the GPU for one host mask; returns (filtered, components)."""
+    import numpy as np
+    m = np.ascontiguousarray(mask, dtype=np.uint8)
+    H, W = m.shape
+    out = np.empty_like(m)
+    nc = ctypes.c_uint64()
+    check(lib().dvc_contour_filter(m.ctypes.data, W, H, int(min_area2), int(device), out.ctypes.data,
+                                   ctypes.byref(nc)))
+    return out, int(nc.value)
+
+
+def gaussian_taps_q8(n: int, sigma: float) -> list:
+    t = (ctypes.c_uint16 * n)()
+    check(lib().dvc_gaussian_taps_q8(n, sigma, t))
+    return list(t)

@@ -1,0 +1,158 @@
+"""One camera feed on one GPU: the per-frame worker of the FD path.
+
+``FDWorker`` owns a ``dvc_fd`` handle (include/dvc.h) and replaces the body of
+the reference loop ``frame_differencing.py:85-138``: ``prime`` is the frame-0
+preprocessing (``fd:67-81``), ``step`` one iteration (``fd:91-133``).
+
+Frames are H x W x 3 uint8 BGR. In host mode they are numpy arrays; in device
+mode (``device_ptrs=True``) they are device buffers — torch tensors on the
+handle's device, or raw integer addresses — and ``step`` is asynchronous.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+
+from . import _native as N
+
+
+def derive_params(width: int, height: int, block_size: int = 4, motion_threshold: float = 0.5,
+                  min_area: float = 500, kernel_size: int = 7, release_factor: float = 0.5,
+                  quantization_level: float = 100, flags: int = 0) -> N.FdParams:
+    """dvc_fd_params from the reference kwargs (frame_differencing.py:21-30).
+
+    * ``ithresh = floor(motion_threshold)`` clamped to [-1, 255]: cv::threshold
+      floors the threshold for 8U input (fd:97).
+    * ``min_area2 = floor(2*min_area)``: ``contourArea > min_area`` is exactly
+      ``2*area > floor(2*min_area)`` for the half-integer polygon areas (fd:103).
+    * addWeighted receives (release_factor, 1 - release_factor, 0) as doubles and
+      computes in float32 (fd:107).
+    """
+    p = N.FdParams()
+    p.width, p.height = int(width), int(height)
+    p.block = int(block_size)
+    p.ithresh = max(-1, min(255, math.floor(motion_threshold)))
+    p.min_area2 = math.floor(2.0 * float(min_area))
+    p.ksize = int(kernel_size)
+    p.anchor = int(kernel_size) // 2
+    p.alpha = float(release_factor)
+    p.beta = float(1 - release_factor)
+    p.gamma = 0.0
+    p.quant = float(quantization_level)
+    p.prime_ksize = 25   # fd:77
+    p.prime_sigma = 30.0
+    p.flags = flags
+    return p
+
+
+def _addr(x) -> int:
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    raise TypeError(f"device mode needs a device tensor or an address, got {type(x)!r}")
+
+
+class FDWorker:
+    def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
+                 device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False, **kwargs):
+        flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
+            | (N.DVC_FLAG_KTIMING if ktiming else 0)
+        self.params = derive_params(width, height, flags=flags, **kwargs)
+        self.W, self.H = int(width), int(height)
+        self.device_ptrs = device_ptrs
+        self._lib = N.lib()
+        h = ctypes.c_void_p()
+        s = ctypes.c_void_p(int(stream)) if stream is not None else None
+        N.check(self._lib.dvc_fd_create(ctypes.byref(self.params), int(device), s, ctypes.byref(h)))
+        self._h = h
+
+    # -------------------------------------------------------------- frames --
+    def _host_frame(self, frame: np.ndarray) -> np.ndarray:
+        if not isinstance(frame, np.ndarray) or frame.dtype != np.uint8 or frame.shape != (self.H, self.W, 3):
+            raise ValueError(f"expected uint8 BGR frame of shape {(self.H, self.W, 3)}")
+        return np.ascontiguousarray(frame)
+
+    def prime(self, frame) -> None:
+        """fd:67-81: previous gray := GaussianBlur(gray(frame), 25x25, 30); acc := 0."""
+        if self.device_ptrs:
+            N.check(self._lib.dvc_fd_prime(self._h, _addr(frame), 3 * self.W))
+        else:
+            f = self._host_frame(frame)
+            N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, 3 * self.W))
+
+    def step(self, frame, overlay=None, compressed=None, acc=None, want=("overlay", "compressed")):
+        """fd:91-133 for one frame.
+
+        Host mode: returns ``(overlay, compressed)`` numpy frames (allocated if
+        not given; a name missing from ``want`` is skipped). Device mode: writes
+        into the given device buffers (None = not produced) and returns None.
+        """
+        if self.device_ptrs:
+            N.check(self._lib.dvc_fd_step(self._h, _addr(frame), 3 * self.W,
+                                          _addr(overlay) if overlay is not None else None,
+                                          _addr(compressed) if compressed is not None else None,
+                                          _addr(acc) if acc is not None else None))
+            return None
+        f = self._host_frame(frame)
+        if overlay is None and "overlay" in want:
+            overlay = np.empty_like(f)
+        if compressed is None and "compressed" in want:
+            compressed = np.empty_like(f)
+        N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, 3 * self.W,
+                                      overlay.ctypes.data if overlay is not None else None,
+                                      compressed.ctypes.data if compressed is not None else None,
+                                      acc.ctypes.data if acc is not None else None))
+        return overlay, compressed
+
+    # -------------------------------------------------------------- graphs --
+    def graph_begin(self) -> None:
+        """Start capturing device-mode steps into a hipGraph (see include/dvc.h)."""
+        N.check(self._lib.dvc_fd_graph_begin(self._h))
+
+    def graph_end(self) -> None:
+        N.check(self._lib.dvc_fd_graph_end(self._h))
+
+    def graph_launch(self) -> None:
+        """Replay the captured frame sequence (asynchronous)."""
+        N.check(self._lib.dvc_fd_graph_launch(self._h))
+
+    # ------------------------------------------------------------- queries --
+    def sync(self) -> None:
+        N.check(self._lib.dvc_fd_sync(self._h))
+
+    def stats(self) -> dict:
+        s = N.FdStats()
+        N.check(self._lib.dvc_fd_get_stats(self._h, ctypes.byref(s)))
+        return {k: int(getattr(s, k)) for k, _ in N.FdStats._fields_}
+
+    def plane(self, which: int) -> np.ndarray:
+        out = np.empty((self.H, self.W), np.uint8)
+        N.check(self._lib.dvc_fd_read_plane(self._h, int(which), out.ctypes.data))
+        return out
+
+    def ktime(self, reset: bool = False):
+        """(total ms, launches) of the dominant (back) kernel, hipEvent-timed."""
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        N.check(self._lib.dvc_fd_ktime(self._h, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0))
+        return float(ms.value), int(n.value)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.dvc_fd_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,180 @@
+/*
+ * dvc.h — C-ABI of the MI355X-native per-frame surveillance-compression worker.
+ *
+ * This is the drop-in boundary for the reference's per-frame hot loop. The
+ * reference (carlozamu/dynamic-video-compression-surveillance, pure Python over
+ * OpenCV 4.11) has no FFI of its own: its per-frame worker is the body of the
+ * loop in
+ *   frame_differencing.py:85-138   filter_and_dilate_movements(...)   (FD path)
+ *   motion_compression_opt.py:65-101, 141-185                          (OF path)
+ * and the Python host (dynamic-video-compression-surveillance_amd/) binds these
+ * symbols with ctypes exactly where the reference calls cv2.* inside that loop.
+ * Each entry point below names the reference lines it replaces.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ *  - Frames are packed 8-bit BGR, H rows of `pitch` bytes (pitch >= 3*W, and a
+ *    multiple of 4), i.e. what cv2.VideoCapture.read() yields (fd:87).
+ *  - Every function returns DVC_OK (0) or a negative DVC_E_* status; the text of
+ *    the last error on the calling thread is available from dvc_last_error().
+ *    The Python host turns a negative status into logging.error(...) and an
+ *    early return, mirroring the reference's try/except (fd:140-145).
+ *  - A handle is single-threaded (one feed, one HIP stream). Distinct handles may
+ *    be driven from distinct host threads concurrently.
+ *  - Unless DVC_FLAG_DEVICE_PTRS is set, frame/output pointers are host memory
+ *    and are staged through pinned buffers owned by the handle; with the flag they
+ *    are device pointers on the handle's device (device-resident benchmark mode).
+ */
+#ifndef DVC_H
+#define DVC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVC_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------- */
+#define DVC_OK             0
+#define DVC_E_INVALID     -1  /* bad argument / unsupported geometry           */
+#define DVC_E_HIP         -2  /* a HIP runtime call failed                     */
+#define DVC_E_STATE       -3  /* call out of order (e.g. step before prime)    */
+#define DVC_E_NOMEM       -4  /* device or pinned allocation failed            */
+#define DVC_E_UNSUPPORTED -5  /* parameter combination not implemented on GPU */
+
+/* ---- flags ----------------------------------------------------------------- */
+#define DVC_FLAG_DEVICE_PTRS 0x1u /* prime/step pointers are device pointers   */
+#define DVC_FLAG_KTIMING     0x2u /* hipEvent-time every launch of the dominant
+                                     (back) kernel; read with dvc_fd_ktime()    */
+#define DVC_FLAG_KEEP_PLANES 0x4u /* keep the filtered / dilated masks of the
+                                     last frame for dvc_fd_read_plane()        */
+
+/* ---- frame-differencing (FD) path ------------------------------------------ */
+
+/*
+ * Parameters, derived on the host from the reference kwargs of
+ * filter_and_dilate_movements (fd:21-30):
+ *   width,height  scaled frame size int(W*scale_factor), int(H*scale_factor) (fd:60-61);
+ *                 frames handed to prime/step are already at this size.
+ *   block         block_size (fd:22); the GPU supports 4 and 8.
+ *   ithresh       floor(motion_threshold): cv::threshold on 8U floors the
+ *                 threshold, so motion = absdiff > ithresh (fd:97).
+ *   min_area2     floor(2*min_area): a contour is kept iff 2*area > min_area2,
+ *                 which is contourArea(c) > min_area exactly, because 2*area of
+ *                 an integer-vertex polygon is an integer (fd:103).
+ *   ksize,anchor  dilation kernel np.ones((k,k)) with OpenCV's default anchor
+ *                 k/2 (fd:80,106). 1 <= ksize <= 63.
+ *   alpha,beta,gamma  addWeighted weights as float32: release_factor,
+ *                 1-release_factor, 0 (fd:107).
+ *   quant         quantization_level as float32 (fd:123).
+ *   prime_ksize,prime_sigma  GaussianBlur of frame 0: 25, 30.0 (fd:77).
+ */
+typedef struct dvc_fd_params {
+    int32_t width;
+    int32_t height;
+    int32_t block;
+    int32_t ithresh;
+    int64_t min_area2;
+    int32_t ksize;
+    int32_t anchor;
+    float alpha;
+    float beta;
+    float gamma;
+    float quant;
+    int32_t prime_ksize;
+    double prime_sigma;
+    uint32_t flags;
+    uint32_t reserved;
+} dvc_fd_params;
+
+/* Cumulative per-handle counters (all frames stepped since create/prime). */
+typedef struct dvc_fd_stats {
+    uint64_t frames;        /* frames stepped                                  */
+    uint64_t motion_px;     /* pixels with absdiff > ithresh                   */
+    uint64_t components;    /* external contours (fill-closed 8-components)    */
+    uint64_t static_blocks; /* blocks whose accumulated mask is all zero       */
+} dvc_fd_stats;
+
+typedef struct dvc_fd dvc_fd;
+
+/* Library / device introspection. */
+int         dvc_abi_version(void);
+const char* dvc_last_error(void);
+int         dvc_device_count(int* count);
+
+/* Create a feed handle on `device`. `hip_stream` (a hipStream_t, may be NULL for
+ * a stream owned by the handle) is the stream every launch of this handle is
+ * enqueued on. Replaces the per-video setup at fd:56-82. */
+int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
+
+/* Frame 0: gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77) -> previous
+ * gray; accumulated mask := 0 (fd:81). Resets the cumulative stats. */
+int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch);
+
+/* One frame of the hot loop, fd:91-133: gray, GaussianBlur 5x5, absdiff,
+ * threshold, findContours/contourArea/drawContours filter, dilate, addWeighted,
+ * red overlay (fd:110-111) and the mask-gated block DCT quantisation with the
+ * YCrCb round trip (fd:115-130). Outputs (each nullable, packed BGR of pitch
+ * out_pitch = 3*W unless noted):
+ *   overlay     the frame written to dilated_motion_mask_video (fd:112)
+ *   compressed  the frame written to compressed_final_video (fd:131)
+ *   acc_out     the accumulated mask after this frame, H*W bytes (fd:107)
+ * The call is asynchronous with respect to the host when DVC_FLAG_DEVICE_PTRS
+ * is set; with host pointers it returns after the outputs have landed. */
+int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch,
+                uint8_t* overlay, uint8_t* compressed, uint8_t* acc_out);
+
+/* Wait for every launch of the handle. */
+int dvc_fd_sync(dvc_fd* h);
+
+/* Read the cumulative counters (synchronises the handle). */
+int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out);
+
+/* Debug/parity access to the internal planes of the LAST stepped frame, each
+ * H*W bytes written to host memory: 0 gray (blurred, fd:93), 1 motion mask
+ * {0,255} (fd:97), 2 filtered mask {0,255} (fd:101-104), 3 accumulated mask
+ * (fd:107), 4 dilated mask {0,255} (fd:106). Planes 2 and 4 need
+ * DVC_FLAG_KEEP_PLANES. Synchronises the handle. */
+#define DVC_PLANE_GRAY     0
+#define DVC_PLANE_MOTION   1
+#define DVC_PLANE_FILTERED 2
+#define DVC_PLANE_ACC      3
+#define DVC_PLANE_DILATED  4
+int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* host_dst);
+
+/* With DVC_FLAG_KTIMING: total milliseconds and launch count of the dominant
+ * kernel since the last reset (synchronises the handle). reset!=0 clears. */
+int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
+
+/* hipGraph capture of a sequence of device-pointer steps (DVC_FLAG_DEVICE_PTRS
+ * only): begin, N x dvc_fd_step, end; each launch replays those N frames (one
+ * graph launch instead of 6N kernel launches). The gray double buffer must be
+ * back in its starting state at the end of the sequence, i.e. N even. */
+int dvc_fd_graph_begin(dvc_fd* h);
+int dvc_fd_graph_end(dvc_fd* h);
+int dvc_fd_graph_launch(dvc_fd* h);
+
+void dvc_fd_destroy(dvc_fd* h);
+
+/* The contour-area filter alone (fd:100-104) on an arbitrary host mask (H*W
+ * bytes, nonzero = foreground): runs the same device kernels as dvc_fd_step
+ * (run extraction, union-find, hole resolution, area, kept-mask paint) and
+ * writes the filtered mask {0,255} to host memory. W, H multiples of 4.
+ * *components (nullable) receives the number of external contours.
+ * Synchronous; for the parity tests. */
+int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_area2,
+                       int device, uint8_t* filtered, uint64_t* components);
+
+/* The Q8 fixed-point Gaussian taps OpenCV's bit-exact 8U GaussianBlur uses
+ * (getGaussianKernelBitExact + error-diffusion rounding to 8 fraction bits).
+ * n odd, 1 <= n <= 63. Exposed for the parity tests. */
+int dvc_gaussian_taps_q8(int n, double sigma, uint16_t* taps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DVC_H */

@@ -1,0 +1,318 @@
+"""CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over ``oracle/liboracle_dvc.so`` (a plain-C restatement of the
+reference's frame-differencing worker, ``frame_differencing.py:67-133``).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker or the CPU baseline. The
+product package (``dynamic-video-compression-surveillance_amd``) never imports
+it and has no CPU fallback.
+
+Parity status: the oracle's numpy-side orchestration is pinned by golden
+vectors captured from the unmodified reference code (``tests/golden/``); its
+OpenCV primitives are restated from OpenCV 4.11's published algorithms and are
+"OCV-unverified" (cv2 is absent from this image) — see DESIGN.md §Parity.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_dvc.so")
+_lib = None
+
+
+class FdParams(ctypes.Structure):
+    """Mirror of ``dvc_fd_params`` (include/dvc.h)."""
+
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("block", ctypes.c_int32),
+        ("ithresh", ctypes.c_int32),
+        ("min_area2", ctypes.c_int64),
+        ("ksize", ctypes.c_int32),
+        ("anchor", ctypes.c_int32),
+        ("alpha", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("gamma", ctypes.c_float),
+        ("quant", ctypes.c_float),
+        ("prime_ksize", ctypes.c_int32),
+        ("prime_sigma", ctypes.c_double),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+class FdStats(ctypes.Structure):
+    _fields_ = [
+        ("frames", ctypes.c_uint64),
+        ("motion_px", ctypes.c_uint64),
+        ("components", ctypes.c_uint64),
+        ("static_blocks", ctypes.c_uint64),
+    ]
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc); returns the .so path."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oc_gauss_kernel_q8.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint16)]
+        L.oc_bgr2gray.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_gaussian_q8.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint16), ctypes.c_int, u8p]
+        L.oc_contour_filter.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, u8p, u8p]
+        L.oc_contour_filter.restype = ctypes.c_int64
+        L.oc_contour_filter_literal.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, u8p]
+        L.oc_contour_filter_literal.restype = ctypes.c_int64
+        L.oc_find_external_contours.argtypes = [u8p, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.POINTER(ctypes.c_int32)),
+                                                ctypes.POINTER(ctypes.POINTER(ctypes.c_int32))]
+        L.oc_find_external_contours.restype = ctypes.c_int64
+        L.oc_contour_area2.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.c_int64]
+        L.oc_contour_area2.restype = ctypes.c_int64
+        L.oc_fill_contour.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                      ctypes.c_int64, ctypes.c_uint8]
+        L.oc_free.argtypes = [ctypes.c_void_p]
+        L.oc_dilate_rect.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_add_weighted_px.argtypes = [ctypes.c_uint8, ctypes.c_float, ctypes.c_uint8, ctypes.c_float, ctypes.c_float]
+        L.oc_add_weighted_px.restype = ctypes.c_uint8
+        L.oc_bgr2ycrcb_px.argtypes = [u8p, u8p]
+        L.oc_ycrcb2bgr_px.argtypes = [u8p, u8p]
+        L.oc_dct_matrix.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        fp = ctypes.POINTER(ctypes.c_float)
+        L.oc_dct2d.argtypes = [fp, ctypes.c_int, fp, fp]
+        L.oc_idct2d.argtypes = [fp, ctypes.c_int, fp, fp]
+        L.oc_block_quant.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                     ctypes.c_float, u8p, ctypes.c_int]
+        L.oc_fd_create.argtypes = [ctypes.POINTER(FdParams), ctypes.c_int]
+        L.oc_fd_create.restype = ctypes.c_void_p
+        L.oc_fd_destroy.argtypes = [ctypes.c_void_p]
+        L.oc_fd_prime.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t]
+        L.oc_fd_step.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, u8p, u8p, u8p]
+        L.oc_fd_read_plane.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p]
+        L.oc_fd_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(FdStats)]
+        _lib = L
+    return _lib
+
+
+def _u8(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+# ---------------------------------------------------------------- params ----
+def fd_params(width, height, block_size=4, motion_threshold=0.5, min_area=500,
+              kernel_size=7, release_factor=0.5, quantization_level=100,
+              prime_ksize=25, prime_sigma=30.0) -> FdParams:
+    """Host-side derivation of dvc_fd_params from the reference kwargs
+    (frame_differencing.py:21-30); same rules as the product's host code."""
+    p = FdParams()
+    p.width, p.height, p.block = int(width), int(height), int(block_size)
+    p.ithresh = max(-1, min(255, math.floor(motion_threshold)))
+    p.min_area2 = math.floor(2.0 * float(min_area))
+    p.ksize = int(kernel_size)
+    p.anchor = int(kernel_size) // 2
+    p.alpha = float(release_factor)
+    p.beta = float(1 - release_factor)
+    p.gamma = 0.0
+    p.quant = float(quantization_level)
+    p.prime_ksize, p.prime_sigma = int(prime_ksize), float(prime_sigma)
+    return p
+
+
+# ------------------------------------------------------------- primitives ----
+def gauss_taps_q8(n: int, sigma: float) -> np.ndarray:
+    t = (ctypes.c_uint16 * n)()
+    if lib().oc_gauss_kernel_q8(n, sigma, t) != 0:
+        raise ValueError("bad kernel size")
+    return np.array(t[:], dtype=np.uint16)
+
+
+def bgr2gray(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr)
+    H, W = bgr.shape[:2]
+    out = np.empty((H, W), np.uint8)
+    lib().oc_bgr2gray(_u8(bgr), W * 3, W, H, _u8(out))
+    return out
+
+
+def gaussian_blur(gray: np.ndarray, n: int, sigma: float) -> np.ndarray:
+    gray = np.ascontiguousarray(gray)
+    H, W = gray.shape
+    k = gauss_taps_q8(n, sigma)
+    kc = (ctypes.c_uint16 * n)(*k.tolist())
+    out = np.empty_like(gray)
+    lib().oc_gaussian_q8(_u8(gray), W, H, kc, n, _u8(out))
+    return out
+
+
+def contour_filter(mask: np.ndarray, min_area2: int, literal: bool = False):
+    """Returns (filtered, n_components[, filled]) — fd:100-104."""
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    H, W = mask.shape
+    out = np.empty_like(mask)
+    if literal:
+        n = lib().oc_contour_filter_literal(_u8(mask), W, H, int(min_area2), _u8(out))
+        return out, int(n)
+    filled = np.empty_like(mask)
+    n = lib().oc_contour_filter(_u8(mask), W, H, int(min_area2), _u8(out), _u8(filled))
+    return out, int(n), filled
+
+
+def find_external_contours(mask: np.ndarray):
+    """Literal Suzuki-Abe RETR_EXTERNAL contours as a list of (N,2) int32 (x,y)."""
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    H, W = mask.shape
+    xy = ctypes.POINTER(ctypes.c_int32)()
+    off = ctypes.POINTER(ctypes.c_int32)()
+    n = lib().oc_find_external_contours(_u8(mask), W, H, ctypes.byref(xy), ctypes.byref(off))
+    offs = np.ctypeslib.as_array(off, shape=(n + 1,)).copy()
+    npts = int(offs[-1])
+    pts = np.ctypeslib.as_array(xy, shape=(max(npts, 1) * 2,)).copy()[: npts * 2].reshape(-1, 2) if npts else np.zeros((0, 2), np.int32)
+    lib().oc_free(ctypes.cast(xy, ctypes.c_void_p))
+    lib().oc_free(ctypes.cast(off, ctypes.c_void_p))
+    return [pts[offs[i]:offs[i + 1]].copy() for i in range(n)]
+
+
+def contour_area2(pts: np.ndarray) -> int:
+    pts = np.ascontiguousarray(pts, dtype=np.int32)
+    return int(lib().oc_contour_area2(pts.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(pts)))
+
+
+def fill_contour(img: np.ndarray, pts: np.ndarray, color: int = 255) -> None:
+    assert img.dtype == np.uint8 and img.flags.c_contiguous
+    pts = np.ascontiguousarray(pts, dtype=np.int32)
+    H, W = img.shape
+    lib().oc_fill_contour(_u8(img), W, H, pts.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(pts), color)
+
+
+def dilate(mask: np.ndarray, k: int, anchor: int | None = None) -> np.ndarray:
+    mask = np.ascontiguousarray(mask)
+    H, W = mask.shape
+    out = np.empty_like(mask)
+    lib().oc_dilate_rect(_u8(mask), W, H, k, k // 2 if anchor is None else anchor, _u8(out))
+    return out
+
+
+def add_weighted(a: np.ndarray, alpha: float, b: np.ndarray, beta: float, gamma: float) -> np.ndarray:
+    f = lib().oc_add_weighted_px
+    out = np.empty_like(a)
+    for i, (x, y) in enumerate(zip(a.ravel().tolist(), b.ravel().tolist())):
+        out.ravel()[i] = f(x, alpha, y, beta, gamma)
+    return out
+
+
+def bgr2ycrcb(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr)
+    out = np.empty_like(bgr)
+    f = lib().oc_bgr2ycrcb_px
+    src, dst = bgr.reshape(-1, 3), out.reshape(-1, 3)
+    for i in range(src.shape[0]):
+        f(_u8(src[i]), _u8(dst[i]))
+    return out
+
+
+def ycrcb2bgr(ycc: np.ndarray) -> np.ndarray:
+    ycc = np.ascontiguousarray(ycc)
+    out = np.empty_like(ycc)
+    f = lib().oc_ycrcb2bgr_px
+    src, dst = ycc.reshape(-1, 3), out.reshape(-1, 3)
+    for i in range(src.shape[0]):
+        f(_u8(src[i]), _u8(dst[i]))
+    return out
+
+
+def dct_matrix(B: int) -> np.ndarray:
+    m = (ctypes.c_float * (B * B))()
+    lib().oc_dct_matrix(B, m)
+    return np.array(m[:], dtype=np.float32).reshape(B, B)
+
+
+def _dct_call(fn, block: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(block, dtype=np.float32)
+    B = x.shape[0]
+    assert x.shape == (B, B) and B in (4, 8)
+    M = dct_matrix(B)
+    y = np.empty_like(x)
+    fp = ctypes.POINTER(ctypes.c_float)
+    fn(x.ctypes.data_as(fp), B, M.ctypes.data_as(fp), y.ctypes.data_as(fp))
+    return y
+
+
+def dct2d(block: np.ndarray) -> np.ndarray:
+    """cv2.dct of a float32 BxB block (orthonormal DCT-II, the oracle's fmaf chain)."""
+    return _dct_call(lib().oc_dct2d, block)
+
+
+def idct2d(block: np.ndarray) -> np.ndarray:
+    """cv2.idct of a float32 BxB block."""
+    return _dct_call(lib().oc_idct2d, block)
+
+
+def block_quant(block: np.ndarray, q: float) -> np.ndarray:
+    """fd:122-125 for one BxB uint8 block of Y."""
+    block = np.ascontiguousarray(block, dtype=np.uint8)
+    B = block.shape[0]
+    M = dct_matrix(B)
+    out = np.empty_like(block)
+    lib().oc_block_quant(_u8(block), B, B, M.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), q, _u8(out), B)
+    return out
+
+
+# ---------------------------------------------------------------- worker ----
+class OracleFD:
+    """The oracle's per-feed worker (fd:67-133), one frame per ``step``."""
+
+    def __init__(self, width, height, literal: bool = False, **kwargs):
+        self.W, self.H = int(width), int(height)
+        self.params = fd_params(width, height, **kwargs)
+        self._h = lib().oc_fd_create(ctypes.byref(self.params), 1 if literal else 0)
+        if not self._h:
+            raise ValueError("oracle rejected parameters")
+
+    def close(self):
+        if self._h:
+            lib().oc_fd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def prime(self, bgr: np.ndarray) -> None:
+        bgr = np.ascontiguousarray(bgr)
+        lib().oc_fd_prime(self._h, _u8(bgr), bgr.shape[1] * 3)
+
+    def step(self, bgr: np.ndarray):
+        bgr = np.ascontiguousarray(bgr)
+        ov = np.empty_like(bgr)
+        cp = np.empty_like(bgr)
+        acc = np.empty(bgr.shape[:2], np.uint8)
+        rc = lib().oc_fd_step(self._h, _u8(bgr), bgr.shape[1] * 3, _u8(ov), _u8(cp), _u8(acc))
+        if rc != 0:
+            raise RuntimeError(f"oracle step failed: {rc}")
+        return ov, cp, acc
+
+    def plane(self, which: int) -> np.ndarray:
+        out = np.empty((self.H, self.W), np.uint8)
+        lib().oc_fd_read_plane(self._h, which, _u8(out))
+        return out
+
+    def stats(self) -> dict:
+        s = FdStats()
+        lib().oc_fd_get_stats(self._h, ctypes.byref(s))
+        return {k: int(getattr(s, k)) for k, _ in FdStats._fields_}

@@ -1,0 +1,201 @@
+"""Capture golden vectors from the UNMODIFIED reference orchestration.
+
+Runs ``/root/reference/frame_differencing.py`` (read-only, imported by path with
+``sys.dont_write_bytecode``) under an in-memory ``cv2`` shim whose primitives
+are the CPU oracle's restatements of OpenCV 4.11 (cv2 itself is absent from
+this image). What this pins: the reference's own numpy-side semantics of the
+per-frame loop (fd:85-138) — mean()==0 block gating, float32 ``/q``,
+``np.round`` half-to-even, ``np.clip``, truncating uint8 slice assignment,
+chroma := 128, the acc>127 overlay, frame bookkeeping — and, through the shim's
+literal Suzuki-Abe findContours / shoelace contourArea / scanline drawContours,
+the contour filter. What it does not pin: the OpenCV primitives themselves
+("OCV-unverified").
+
+Container-only (needs /root/reference); the outputs are committed as small
+fixtures under tests/golden/ and the GPU box never reads the reference.
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import importlib.util
+import json
+import math
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import oracle as O  # noqa: E402
+from dvc_amd.synthetic import clip  # noqa: E402
+
+REF = "/root/reference/frame_differencing.py"
+
+
+# ------------------------------------------------------------------ shim ----
+def make_cv2(clips: dict, written: dict) -> types.ModuleType:
+    cv2 = types.ModuleType("cv2")
+    cv2.CAP_PROP_FPS, cv2.CAP_PROP_FRAME_WIDTH, cv2.CAP_PROP_FRAME_HEIGHT = 5, 3, 4
+    cv2.COLOR_BGR2GRAY, cv2.COLOR_BGR2YCrCb, cv2.COLOR_YCrCb2BGR = 6, 36, 38
+    cv2.THRESH_BINARY, cv2.RETR_EXTERNAL, cv2.CHAIN_APPROX_SIMPLE, cv2.FILLED = 0, 0, 2, -1
+
+    class VideoCapture:
+        def __init__(self, path):
+            self.f = clips.get(path)
+            self.i = 0
+
+        def isOpened(self):
+            return self.f is not None
+
+        def get(self, prop):
+            return {5: 25.0, 3: float(self.f.shape[2]), 4: float(self.f.shape[1])}.get(prop, 0.0)
+
+        def read(self):
+            if self.i >= len(self.f):
+                return False, None
+            fr = self.f[self.i].copy()
+            self.i += 1
+            return True, fr
+
+        def release(self):
+            pass
+
+    class VideoWriter:
+        def __init__(self, path, fourcc, fps, size, isColor=True):
+            self.name = os.path.basename(path)
+            written[self.name] = []
+
+        def write(self, frame):
+            written[self.name].append(np.array(frame, copy=True))
+
+        def release(self):
+            pass
+
+    cv2.VideoCapture = VideoCapture
+    cv2.VideoWriter = VideoWriter
+    cv2.VideoWriter_fourcc = lambda *a: 0
+
+    def resize(img, size):
+        if tuple(size) != (img.shape[1], img.shape[0]):
+            raise NotImplementedError("golden capture runs at scale 1.0")
+        return img.copy()
+
+    def cvtColor(img, code):
+        if code == cv2.COLOR_BGR2GRAY:
+            return O.bgr2gray(img)
+        if code == cv2.COLOR_BGR2YCrCb:
+            return O.bgr2ycrcb(img)
+        if code == cv2.COLOR_YCrCb2BGR:
+            return O.ycrcb2bgr(img)
+        raise ValueError(code)
+
+    def GaussianBlur(img, ksize, sigma):
+        assert ksize[0] == ksize[1]
+        return O.gaussian_blur(img, int(ksize[0]), float(sigma))
+
+    def absdiff(a, b):
+        return np.abs(a.astype(np.int16) - b.astype(np.int16)).astype(np.uint8)
+
+    def threshold(src, thresh, maxval, typ):
+        assert typ == cv2.THRESH_BINARY and src.dtype == np.uint8
+        it = math.floor(thresh)  # cv::threshold floors the threshold for 8U
+        if it < 0:
+            return float(it), np.full_like(src, 255)
+        return float(it), np.where(src > it, np.uint8(maxval), np.uint8(0)).astype(np.uint8)
+
+    def findContours(img, mode, method):
+        cs = O.find_external_contours(img)
+        return tuple(c.reshape(-1, 1, 2).astype(np.int32) for c in cs), None
+
+    def contourArea(c):
+        return O.contour_area2(np.asarray(c).reshape(-1, 2)) / 2.0
+
+    def drawContours(img, contours, idx, color, thickness):
+        assert idx == -1 and thickness == cv2.FILLED
+        for c in contours:
+            O.fill_contour(img, np.asarray(c).reshape(-1, 2), int(color))
+        return img
+
+    def dilate(img, kernel, iterations=1):
+        assert iterations == 1 and kernel.shape[0] == kernel.shape[1] and kernel.all()
+        return O.dilate(img, kernel.shape[0])
+
+    def addWeighted(a, alpha, b, beta, gamma):
+        # saturate_cast<uchar>(fma(a, (float)alpha, fma(b, (float)beta, (float)gamma)));
+        # float64 products of float32 operands are exact and so are these sums
+        al, be, ga = np.float32(alpha), np.float32(beta), np.float32(gamma)
+        inner = (b.astype(np.float64) * np.float64(be) + np.float64(ga)).astype(np.float32)
+        t = (a.astype(np.float64) * np.float64(al) + inner.astype(np.float64)).astype(np.float32)
+        return np.clip(np.rint(t), 0, 255).astype(np.uint8)
+
+    def split(img):
+        return tuple(np.ascontiguousarray(img[:, :, c]) for c in range(img.shape[2]))
+
+    def merge(chs):
+        return np.stack(chs, axis=-1)
+
+    def dct(block):
+        return O.dct2d(block)
+
+    def idct(block):
+        return O.idct2d(block)
+
+    for fn in (resize, cvtColor, GaussianBlur, absdiff, threshold, findContours, contourArea, drawContours,
+               dilate, addWeighted, split, merge, dct, idct):
+        setattr(cv2, fn.__name__, fn)
+    return cv2
+
+
+def run_reference(frames: np.ndarray, **kwargs):
+    clips = {"clip.mp4": frames}
+    written: dict = {}
+    sys.modules["cv2"] = make_cv2(clips, written)
+    spec = importlib.util.spec_from_file_location("ref_frame_differencing", REF)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with tempfile.TemporaryDirectory() as td:
+        mod.filter_and_dilate_movements("clip.mp4", td, **kwargs)
+        times = open(os.path.join(td, "clip", "execution_times.txt")).read()
+    del sys.modules["cv2"]
+    ov = np.stack(written["dilated_motion_mask_video.mp4"])
+    cp = np.stack(written["compressed_final_video.mp4"])
+    return ov, cp, times
+
+
+from tests.golden.cases import CASES, FULL_ARRAYS  # noqa: E402
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main():
+    arrays, meta = {}, {}
+    for name, (mk, kw) in CASES.items():
+        frames = mk()
+        ov, cp, times = run_reference(frames, **kw)
+        assert ov.shape == (len(frames) - 1,) + frames.shape[1:], ov.shape
+        assert times.splitlines()[1] == f"  Frames processed: {len(frames) - 1}"
+        if name in FULL_ARRAYS:  # small cases keep every output pixel (diffable)
+            arrays[f"{name}__overlay"] = ov
+            arrays[f"{name}__compressed"] = cp
+        meta[name] = {"kwargs": kw, "n_frames": int(len(frames)), "input_sha256": [sha(f) for f in frames],
+                      "overlay_sha256": [sha(f) for f in ov], "compressed_sha256": [sha(f) for f in cp]}
+        print(f"{name}: {len(frames)} frames, kwargs={kw}")
+    np.savez_compressed(os.path.join(HERE, "fd_golden.npz"), **arrays)
+    with open(os.path.join(HERE, "fd_golden.json"), "w") as f:
+        json.dump({"cases": meta,
+                   "source": "reference frame_differencing.py:21-159 under tests/golden/make_golden.py cv2 shim"},
+                  f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+"""GPU parity: the HIP frame-differencing path vs the CPU oracle, through the C-ABI.
+
+Bar (BASELINE.json north_star): uint8 motion/filtered/dilated/accumulated masks
+bit-exact; overlay and compressed frames bit-exact as well (the DCT runs the
+same float32 fmaf chain as the oracle, so no tolerance is needed against it).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PLANES = {"gray": 0, "motion": 1, "filtered": 2, "acc": 3, "dilated": 4}
+
+
+def _run_pair(dvc_amd, oracle, frames, **kw):
+    H, W = frames.shape[1:3]
+    gpu = dvc_amd.FDWorker(W, H, device=0, keep_planes=True, **kw)
+    ref = oracle.OracleFD(W, H, **kw)
+    gpu.prime(frames[0])
+    ref.prime(frames[0])
+    for t in range(1, len(frames)):
+        ov, cp = gpu.step(frames[t])
+        rov, rcp, racc = ref.step(frames[t])
+        for name, idx in PLANES.items():
+            g, r = gpu.plane(idx), ref.plane(idx)
+            if not np.array_equal(g, r):
+                d = np.argwhere(g != r)
+                raise AssertionError(f"{name} plane differs at frame {t}: {len(d)} px, first {d[:5].tolist()}")
+        assert np.array_equal(ov, rov), f"overlay differs at frame {t}: {(ov != rov).any(-1).sum()} px"
+        if not np.array_equal(cp, rcp):
+            diff = np.abs(cp.astype(int) - rcp.astype(int))
+            raise AssertionError(f"compressed differs at frame {t}: {(diff > 0).any(-1).sum()} px, max {diff.max()}")
+    gs, rs = gpu.stats(), ref.stats()
+    assert gs == rs, (gs, rs)
+    gpu.close()
+    ref.close()
+    return gs
+
+
+@pytest.mark.parametrize("W,H,n,seed,noisy", [
+    (640, 360, 12, 0, False),
+    (640, 360, 8, 5, True),
+    (1920, 1080, 4, 1, False),
+    (1920, 1080, 3, 2, True),
+    (3840, 2160, 3, 4, False),
+])
+def test_fd_parity_synthetic(gpu_lib, oracle_lib, W, H, n, seed, noisy):
+    from dvc_amd.synthetic import clip
+    st = _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=seed, noisy=noisy))
+    assert st["frames"] == n - 1
+
+
+def test_fd_parity_main_variant(gpu_lib, oracle_lib):
+    """frame_differencing.py:200-207 kwargs (block 8, kernel 10 = asymmetric anchor, release 0.3)."""
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(640, 360, 8, seed=7), block_size=8, kernel_size=10,
+              release_factor=0.3, quantization_level=100)
+
+
+def test_fd_parity_random_frames(gpu_lib, oracle_lib):
+    """Pure-noise frames: frame 1 is one giant component riddled with holes."""
+    rng = np.random.default_rng(11)
+    frames = rng.integers(0, 256, (5, 96, 160, 3), dtype=np.uint8)
+    _run_pair(gpu_lib, oracle_lib, frames)
+
+
+def test_fd_parity_thresholds(gpu_lib, oracle_lib):
+    from dvc_amd.synthetic import clip
+    frames = clip(320, 240, 6, seed=9, noisy=True)
+    for thr, ma in [(-1.0, 0), (3.7, 50), (254.5, 500), (0.5, -1)]:
+        _run_pair(gpu_lib, oracle_lib, frames, motion_threshold=thr, min_area=ma)
+
+
+def _masks():
+    rng = np.random.default_rng(123)
+    out = []
+    for H, W, p in [(16, 16, 0.5), (64, 64, 0.3), (40, 132, 0.55), (100, 200, 0.45), (8, 256, 0.5),
+                    (128, 68, 0.6), (200, 300, 0.1)]:
+        out.append((rng.random((H, W)) < p).astype(np.uint8) * 255)
+    m = np.zeros((120, 160), np.uint8)                # nested rings + holes + border contact
+    for r0, v in [(2, 255), (10, 0), (18, 255), (26, 0), (34, 255)]:
+        m[r0:120 - r0, r0:160 - r0] = v
+    m[0:5, 100:140] = 255
+    out.append(m)
+    out.append(np.full((64, 64), 255, np.uint8))    # everything
+    out.append(np.zeros((64, 64), np.uint8))        # nothing
+    cb = (np.indices((48, 128)).sum(0) % 2 * 255).astype(np.uint8)  # checkerboard: max runs per row
+    out.append(cb)
+    tall = np.zeros((1080, 64), np.uint8)            # tall components: deep union-find chains
+    tall[:, 10:14] = 255
+    tall[:, 30] = 255
+    tall[::2, 40:50] = 255
+    out.append(tall)
+    stripes = np.zeros((64, 4096), np.uint8)         # wide rows
+    stripes[:, ::3] = 255
+    out.append(stripes)
+    return out
+
+
+def test_contour_filter_masks(gpu_lib, oracle_lib):
+    for i, m in enumerate(_masks()):
+        for ma2 in (-1, 0, 6, 1000):
+            g, gn = gpu_lib._native.contour_filter(m, ma2)
+            r, rn, _ = oracle_lib.contour_filter(m, ma2)
+            assert gn == rn, (i, ma2, gn, rn)
+            assert np.array_equal(g, r), (i, ma2, int((g != r).sum()))
+
+
+def test_contour_filter_random_sweep(gpu_lib, oracle_lib):
+    rng = np.random.default_rng(5)
+    for _ in range(60):
+        H, W = 4 * int(rng.integers(1, 40)), 4 * int(rng.integers(1, 60))
+        m = (rng.random((H, W)) < rng.uniform(0.05, 0.9)).astype(np.uint8) * 255
+        ma2 = int(rng.integers(-1, 40))
+        g, gn = gpu_lib._native.contour_filter(m, ma2)
+        r, rn, _ = oracle_lib.contour_filter(m, ma2)
+        assert gn == rn and np.array_equal(g, r), (H, W, ma2)
+
+
+def test_device_mode_matches_host_mode(gpu_lib):
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = clip(640, 360, 6, seed=2)
+    host = gpu_lib.FDWorker(640, 360)
+    host.prime(frames[0])
+    outs = [host.step(f) for f in frames[1:]]
+    dev = torch.from_numpy(frames).to("cuda:0")
+    ov = torch.empty_like(dev[0])
+    cp = torch.empty_like(dev[0])
+    acc = torch.empty((360, 640), dtype=torch.uint8, device="cuda:0")
+    w = gpu_lib.FDWorker(640, 360, device_ptrs=True, stream=torch.cuda.current_stream().cuda_stream)
+    w.prime(dev[0])
+    for t in range(1, 6):
+        w.step(dev[t], ov, cp, acc)
+        torch.cuda.synchronize()
+        assert np.array_equal(ov.cpu().numpy(), outs[t - 1][0])
+        assert np.array_equal(cp.cpu().numpy(), outs[t - 1][1])
+    w.close()
+    host.close()
+
+
+def test_graph_replay_matches_eager(gpu_lib):
+    """hipGraph capture of an even frame sequence == the same steps launched eagerly."""
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = torch.from_numpy(clip(640, 360, 5, seed=4)).to("cuda:0")
+    order = [1, 2, 3, 4, 3, 2]          # ping-pong after frame 0
+    outs = []
+    for use_graph in (False, True):
+        ov = torch.empty((len(order), 360, 640, 3), dtype=torch.uint8, device="cuda:0")
+        cp = torch.empty_like(ov)
+        w = gpu_lib.FDWorker(640, 360, device_ptrs=True)
+        w.prime(frames[0])
+        if use_graph:
+            w.graph_begin()
+        for j, t in enumerate(order):
+            w.step(frames[t], ov[j], cp[j])
+        if use_graph:
+            w.graph_end()
+            w.graph_launch()
+            w.graph_launch()      # second pass: state carries over exactly as eager would
+        else:
+            for j, t in enumerate(order):
+                w.step(frames[t], ov[j], cp[j])
+        w.sync()
+        outs.append((ov.cpu().numpy(), cp.cpu().numpy(), w.stats()))
+        w.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+
+
+def test_errors(gpu_lib):
+    from dvc_amd._native import DvcError
+    with pytest.raises(DvcError):
+        gpu_lib.FDWorker(642, 360)            # not a multiple of the block
+    with pytest.raises(DvcError):
+        gpu_lib.FDWorker(640, 360, block_size=16)
+    w = gpu_lib.FDWorker(640, 360)
+    with pytest.raises(DvcError):
+        w.step(np.zeros((360, 640, 3), np.uint8))   # step before prime
+    w.close()
+
+
+def test_process_single_video_fd(gpu_lib, tmp_path):
+    from dvc_amd.frame_differencing import process_single_video_fd
+    calls = []
+    process_single_video_fd("synthetic://320x240?frames=102&seed=3", str(tmp_path), progress_callback=calls.append)
+    d = tmp_path / "320x240"
+    assert calls == [50, 100]
+    ov = np.load(d / "dilated_motion_mask_video.npy")
+    cp = np.load(d / "compressed_final_video.npy")
+    assert ov.shape == (101, 240, 320, 3) and cp.shape == ov.shape
+    txt = (d / "execution_times.txt").read_text().splitlines()
+    assert txt[0] == "Frame Differencing:" and txt[1] == "  Frames processed: 101"
+    assert (d / "processing.log").exists()
