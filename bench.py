@@ -86,6 +86,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch per frame instead of replaying a hipGraph")
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="frames in flight (contour filter of consecutive frames on concurrent HIP streams); "
+                         "must divide the 126-frame step")
     args = ap.parse_args()
 
     import numpy as np
@@ -115,7 +118,7 @@ def main():
     torch.cuda.synchronize()
 
     def make_worker(ktiming=False):
-        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming)
+        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming, pipeline=args.pipeline)
         w.prime(ring[0])
         return w
 
@@ -191,6 +194,7 @@ def main():
             "config": {"workload": "fd_1080p_single_feed_per_gpu" if (W, H) == (1920, 1080) else f"fd_{W}x{H}",
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": 1,
                        "ring_frames": R, "noisy": args.noisy, "launch": "hipgraph" if graph else "eager",
+                       "frames_in_flight": args.pipeline,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
                        "pipeline_bytes_per_px": PIPE_BYTES_PER_PX,

@@ -58,7 +58,7 @@ class FdParams(ctypes.Structure):
         ("prime_ksize", ctypes.c_int32),
         ("prime_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("pipeline", ctypes.c_uint32),
     ]
 
 

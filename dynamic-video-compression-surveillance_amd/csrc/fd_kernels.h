@@ -32,7 +32,8 @@ struct CclBufs {
     uint32_t* gpar;         // 1 + H x (CAP+1) gap parents, node 0 = outside
     uint8_t* gE;            // H x (CAP+1) gap is outside (1) / hole (0)
     uint32_t* area2;        // H x CAP 2*area per root
-    unsigned long long* stats;
+    uint64_t* kbits;        // H x WW kept (filtered) mask
+    unsigned long long* stats;  // 64 slots x 4 counters
 };
 
 struct BackArgs {
@@ -43,17 +44,11 @@ struct BackArgs {
     uint8_t* overlay;     // nullable
     uint8_t* compressed;  // nullable
     int opitch;
-    const uint16_t *rs, *re;
-    const uint32_t* nfg;
-    const uint32_t* fpar;
-    const uint8_t* gE;
-    const uint32_t* area2;
-    int64_t min_area2;
+    const uint64_t* kbits;  // kept (filtered) mask from k_paint
     int ksize, anchor;
     float alpha, beta, gamma, quant;
     DctMat M;
     unsigned long long* stats;
-    uint64_t* dbg_kept;  // nullable: kept (filtered) mask bits
     uint64_t* dbg_dil;   // nullable: dilated mask bits
 };
 
@@ -61,7 +56,8 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
                         int W, int H, const GaussTaps& k, hipStream_t s);
 hipError_t launch_front(const uint8_t* bgr, int pitch, const uint8_t* prev, uint8_t* cur, uint64_t* mbits,
                         const RowGeom& g, int ithresh, hipStream_t s);
-hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, hipStream_t s);
+int band_rows(const RowGeom& g);
+hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int64_t min_area2, hipStream_t s);
 hipError_t launch_back(const BackArgs& a, int block, hipStream_t s);
 
 }  // namespace dvc

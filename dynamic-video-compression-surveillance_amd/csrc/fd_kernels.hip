@@ -1,21 +1,24 @@
 // fd_kernels.hip — gfx950 (MI355X / CDNA4) kernels of the frame-differencing
 // per-frame worker (reference: frame_differencing.py:85-138).
 //
-// One frame = six launches on the feed's stream:
+// One frame = seven launches on the feed's stream:
 //   k_front   BGR->gray (fd:92), 5x5 Q8 Gaussian (fd:93), absdiff+threshold
 //             (fd:96-97) -> new gray plane + 1-bit motion mask (64 px / u64)
-//   k_runs    per row: maximal foreground runs + background gaps of the bit mask;
-//             union-find init (border gaps linked to the OUTSIDE node 0)
-//   k_union   per row pair: foreground runs 8-connected, gaps 4-connected
+//   k_band    per band of rows, one workgroup: maximal foreground runs and
+//             background gaps of every row straight from the bit mask, then
+//             union-find in LDS (runs 8-connected, gaps 4-connected, border gaps
+//             joined to the OUTSIDE node) -> band-local roots as global ids
+//   k_merge   per band seam: global unions of band roots (atomicMin links)
 //   k_resolve gaps reaching node 0 are outside (E); the rest are holes: hole
 //             pixels are painted into the filled mask F = not E, and the runs
 //             left/right of a hole are united (nested components join the
 //             external component that encloses them)
 //   k_area    2*contourArea of every external component from F's 2x2 windows,
 //             accumulated per root (fd:100-103)
-//   k_back    kept components painted (drawContours FILLED, fd:104), 7x7 dilate
-//             (fd:106), addWeighted (fd:107), red overlay (fd:110-111), static
-//             BxB block DCT quantisation + YCrCb round trip (fd:115-130)
+//   k_paint   kept components -> filtered bit mask (drawContours FILLED, fd:104)
+//   k_back    7x7 dilate (fd:106), addWeighted (fd:107), red overlay
+//             (fd:110-111), static BxB block DCT quantisation + YCrCb round trip
+//             (fd:115-130)
 //
 // Everything is integer/byte work except the addWeighted rint and the block
 // DCT (fp32, explicit fmaf chains — compiled with -ffp-contract=off).
@@ -26,6 +29,11 @@
 #include "fd_kernels.h"
 
 namespace dvc {
+
+// Cumulative counters live in 64 slots x 4 (frames, motion px, components,
+// static blocks) so concurrent workgroups do not all hit one address; the host
+// sums the slots.
+#define STAT_SLOT(i) ((unsigned)(i) & 63u)
 
 // ---------------------------------------------------------------- helpers ---
 __device__ __forceinline__ int reflect101(int x, int n)
@@ -172,7 +180,10 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 // ------------------------------------------------------------------ front ---
 // Tile: 256 px (64 lanes x 4 px) x 16 rows; 4 waves. Gray halo 2 px / 2 rows,
 // loaded as 66 quads x 20 rows with BORDER_REFLECT_101 at the image edges.
+// Every BGR and previous-gray load of a thread is issued before the first use
+// (fully unrolled), so a workgroup keeps ~6 KB of HBM reads in flight.
 constexpr int FT_W = 256, FT_H = 16, FT_Q = FT_W / 4 + 2, FT_R = FT_H + 4;
+constexpr int FT_ITEMS = FT_R * FT_Q, FT_NIT = (FT_ITEMS + 255) / 256;
 
 __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, int pitch,
                                                const uint8_t* __restrict__ prev, uint8_t* __restrict__ cur,
@@ -182,58 +193,93 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H;
+    const int x = x0 + 4 * lane;
 
-    for (int it = tid; it < FT_R * FT_Q; it += 256) {
-        int r = it / FT_Q, qq = it - r * FT_Q;
-        int gy = reflect101(y0 - 2 + r, H);
-        int gx = x0 + 4 * (qq - 1);
-        const uint8_t* row = bgr + (size_t)gy * pitch;
-        uint32_t v;
-        if (gx >= 0 && gx + 3 < W) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(row + 3 * gx);
-            v = gray4(p[0], p[1], p[2]);
-        } else {
-            v = 0;
-            for (int i = 0; i < 4; ++i) {
-                int sx = reflect101(gx + i, W);
-                const uint8_t* s = row + 3 * sx;
-                v |= gray_px(s[0], s[1], s[2]) << (8 * i);
+    // previous gray of this lane's 4 output rows (independent of everything else)
+    uint32_t pv[FT_H / 4];
+#pragma unroll
+    for (int i = 0; i < FT_H / 4; ++i) {
+        const int y = y0 + wave + 4 * i;
+        pv[i] = (y < H && x < W) ? *reinterpret_cast<const uint32_t*>(prev + (size_t)y * W + x) : 0u;
+    }
+    uint32_t v0[FT_NIT], v1[FT_NIT], v2[FT_NIT];
+#pragma unroll
+    for (int i = 0; i < FT_NIT; ++i) {
+        const int it = tid + 256 * i;
+        v0[i] = v1[i] = v2[i] = 0;
+        if (it < FT_ITEMS) {
+            const int r = it / FT_Q, qq = it - r * FT_Q;
+            int gy = y0 - 2 + r;
+            if (gy < 0 || gy >= H) gy = reflect101(gy, H);
+            const int gx = x0 + 4 * (qq - 1);
+            if (gx >= 0 && gx + 3 < W) {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(bgr + (size_t)gy * pitch + 3 * gx);
+                v0[i] = p[0];
+                v1[i] = p[1];
+                v2[i] = p[2];
             }
         }
-        sg[r][qq] = v;
     }
-    __syncthreads();
-
-    for (int it = tid; it < FT_R * (FT_W / 4); it += 256) {
-        int r = it >> 6, q = it & 63;
-        uint32_t a = sg[r][q], b = sg[r][q + 1], c = sg[r][q + 2];
-        uint32_t p[8] = {(a >> 16) & 255, a >> 24, b & 255, (b >> 8) & 255, (b >> 16) & 255, b >> 24, c & 255, (c >> 8) & 255};
-        uint32_t h[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) h[i] = p[i] + 4 * p[i + 1] + 6 * p[i + 2] + 4 * p[i + 3] + p[i + 4];
-        sh[r][q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    for (int i = 0; i < FT_NIT; ++i) {
+        const int it = tid + 256 * i;
+        if (it < FT_ITEMS) {
+            const int r = it / FT_Q, qq = it - r * FT_Q;
+            const int gx = x0 + 4 * (qq - 1);
+            uint32_t gq;
+            if (gx >= 0 && gx + 3 < W) {
+                gq = gray4(v0[i], v1[i], v2[i]);
+            } else if (gx >= W + 2) {
+                gq = 0;  // beyond every 5-tap window of an in-image pixel: never read
+            } else {  // image edge: BORDER_REFLECT_101 per pixel
+                int gy = y0 - 2 + r;
+                if (gy < 0 || gy >= H) gy = reflect101(gy, H);
+                const uint8_t* row = bgr + (size_t)gy * pitch;
+                gq = 0;
+                for (int j = 0; j < 4; ++j) {
+                    const uint8_t* s = row + 3 * reflect101(gx + j, W);
+                    gq |= gray_px(s[0], s[1], s[2]) << (8 * j);
+                }
+            }
+            sg[r][qq] = gq;
+        }
     }
     __syncthreads();
 
-    const int x = x0 + 4 * lane;
-    for (int rr = wave; rr < FT_H; rr += 4) {
-        const int y = y0 + rr;
-        uint2 v0 = sh[rr][lane], v1 = sh[rr + 1][lane], v2 = sh[rr + 2][lane], v3 = sh[rr + 3][lane], v4 = sh[rr + 4][lane];
-        uint32_t lo0 = (v0.x & 0xffff) + 4 * (v1.x & 0xffff) + 6 * (v2.x & 0xffff) + 4 * (v3.x & 0xffff) + (v4.x & 0xffff);
-        uint32_t lo1 = (v0.x >> 16) + 4 * (v1.x >> 16) + 6 * (v2.x >> 16) + 4 * (v3.x >> 16) + (v4.x >> 16);
-        uint32_t lo2 = (v0.y & 0xffff) + 4 * (v1.y & 0xffff) + 6 * (v2.y & 0xffff) + 4 * (v3.y & 0xffff) + (v4.y & 0xffff);
-        uint32_t lo3 = (v0.y >> 16) + 4 * (v1.y >> 16) + 6 * (v2.y >> 16) + 4 * (v3.y >> 16) + (v4.y >> 16);
-        uint32_t g = ((lo0 + 128) >> 8) | (((lo1 + 128) >> 8) << 8) | (((lo2 + 128) >> 8) << 16) | (((lo3 + 128) >> 8) << 24);
+#pragma unroll
+    for (int i = 0; i < (FT_R * 64 + 255) / 256; ++i) {
+        const int it = tid + 256 * i;
+        if (it < FT_R * 64) {
+            const int r = it >> 6, q = it & 63;
+            const uint32_t a = sg[r][q], b = sg[r][q + 1], c = sg[r][q + 2];
+            const uint32_t p[8] = {(a >> 16) & 255, a >> 24, b & 255, (b >> 8) & 255, (b >> 16) & 255, b >> 24,
+                                   c & 255, (c >> 8) & 255};
+            uint32_t h[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) h[j] = p[j] + 4 * p[j + 1] + 6 * p[j + 2] + 4 * p[j + 3] + p[j + 4];
+            sh[r][q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        }
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int i = 0; i < FT_H / 4; ++i) {
+        const int rr = wave + 4 * i, y = y0 + rr;
+        const uint2 a0 = sh[rr][lane], a1 = sh[rr + 1][lane], a2 = sh[rr + 2][lane], a3 = sh[rr + 3][lane],
+                    a4 = sh[rr + 4][lane];
+        // 16-bit lanes: sum <= 16 * 4080 = 65280, packed adds cannot carry across halves
+        const uint32_t sx = a0.x + 4 * a1.x + 6 * a2.x + 4 * a3.x + a4.x;
+        const uint32_t sy = a0.y + 4 * a1.y + 6 * a2.y + 4 * a3.y + a4.y;
+        const uint32_t g = (((sx & 0xffff) + 128) >> 8) | ((((sx >> 16) + 128) >> 8) << 8) |
+                           ((((sy & 0xffff) + 128) >> 8) << 16) | ((((sy >> 16) + 128) >> 8) << 24);
         uint32_t nib = 0;
         if (y < H && x < W) {
-            size_t o = (size_t)y * W + x;
-            *reinterpret_cast<uint32_t*>(cur + o) = g;
-            uint32_t pv = *reinterpret_cast<const uint32_t*>(prev + o);
+            *reinterpret_cast<uint32_t*>(cur + (size_t)y * W + x) = g;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                int a = (g >> (8 * i)) & 255, b = (pv >> (8 * i)) & 255;
-                int d = a > b ? a - b : b - a;
-                nib |= (uint32_t)(d > ithresh) << i;
+            for (int j = 0; j < 4; ++j) {
+                const int da = (g >> (8 * j)) & 255, db = (pv[i] >> (8 * j)) & 255;
+                const int d = da > db ? da - db : db - da;
+                nib |= (uint32_t)(d > ithresh) << j;
             }
         }
         unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
@@ -241,101 +287,204 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
         w |= __shfl_xor(w, 2, 64);
         w |= __shfl_xor(w, 4, 64);
         w |= __shfl_xor(w, 8, 64);
-        int wi = (x0 >> 6) + (lane >> 4);
+        const int wi = (x0 >> 6) + (lane >> 4);
         if ((lane & 15) == 0 && y < H && wi < WW) mbits[(size_t)y * WW + wi] = w;
     }
 }
 
-// ------------------------------------------------------------------- runs ---
-// One wave (64-thread block) per row. Dynamic LDS: 2*CAP u16.
-__global__ void __launch_bounds__(64) k_runs(const uint64_t* __restrict__ mbits, RowGeom g,
-                                             uint16_t* __restrict__ rs, uint16_t* __restrict__ re,
-                                             uint32_t* __restrict__ nfg, uint32_t* __restrict__ fpar,
-                                             uint32_t* __restrict__ gpar, uint32_t* __restrict__ area2,
-                                             unsigned long long* __restrict__ stats)
+// ------------------------------------------------------------------- band ---
+// One workgroup per band of BH rows (one wave per row): extract the row's
+// foreground runs straight from the bit mask, then union-find in LDS over the
+// band's runs (8-connected) and gaps (4-connected; gaps on the image border
+// joined to the OUTSIDE node), flatten, and publish every run/gap's band-local
+// root as a global id. Local ids: 0 = OUTSIDE, fg (r,k) = 1 + r*CAP + k,
+// gap (r,k) = 1 + BH*CAP + r*(CAP+1) + k. Dynamic LDS: local parents.
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p)
 {
-    extern __shared__ __attribute__((aligned(16))) uint16_t s_runs[];
-    uint16_t* s_rs = s_runs;
-    uint16_t* s_re = s_runs + g.CAP;
-    const int y = blockIdx.x, lane = threadIdx.x;
-    const uint64_t* row = mbits + (size_t)y * g.WW;
-    int ns = 0, ne = 0;
-    unsigned long long motion = 0;
-    for (int base = 0; base < g.WW; base += 64) {
-        int i = base + lane;
-        uint64_t w = 0, pw = 0, nw = 0;
-        if (i < g.WW) {
-            w = row[i];
-            pw = i > 0 ? row[i - 1] : 0;
-            nw = i + 1 < g.WW ? row[i + 1] : 0;
-        }
-        uint64_t st = w & ~((w << 1) | (pw >> 63));
-        uint64_t en = w & ~((w >> 1) | (nw << 63));
-        int cs = __popcll(st), ce = __popcll(en);
-        int ps = wave_incl_scan(cs), pe = wave_incl_scan(ce);
-        int ks = ns + ps - cs, ke = ne + pe - ce;
-        while (st) { int b = __ffsll((unsigned long long)st) - 1; s_rs[ks++] = (uint16_t)(i * 64 + b); st &= st - 1; }
-        while (en) { int b = __ffsll((unsigned long long)en) - 1; s_re[ke++] = (uint16_t)(i * 64 + b); en &= en - 1; }
-        ns += __shfl(ps, 63, 64);
-        ne += __shfl(pe, 63, 64);
-        motion += (unsigned long long)__popcll(w);
-    }
-    __syncthreads();
-    const int n = ns;
-    const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
-    for (int k = lane; k < n; k += 64) {
-        rs[base + k] = s_rs[k];
-        re[base + k] = s_re[k];
-        fpar[base + k] = base + k;
-        area2[base + k] = 0;
-    }
-    for (int k = lane; k <= n; k += 64) {
-        int a = k == 0 ? 0 : (int)s_re[k - 1] + 1;
-        int b = k == n ? g.W - 1 : (int)s_rs[k] - 1;
-        bool border = (y == 0 || y == g.H - 1 || a == 0 || b == g.W - 1);
-        gpar[gbase + k] = (a <= b && border) ? 0u : gbase + k;
-    }
-    if (lane == 0) nfg[y] = (uint32_t)n;
-    if (y == 0 && lane == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
-    // motion pixel count: one atomic per row
-    for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);
-    if (lane == 0 && motion) atomicAdd(stats + 1, motion);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// ------------------------------------------------------------------ union ---
-// One wave per row pair (y, y+1). Dynamic LDS: 4*CAP u16.
-__global__ void __launch_bounds__(64) k_union(RowGeom g, const uint16_t* __restrict__ rs,
+__device__ uint32_t lfind(uint32_t* lp, uint32_t x)
+{
+    for (;;) {
+        uint32_t p = lds_ld(lp + x);
+        if (p == x) return x;
+        uint32_t gp = lds_ld(lp + p);
+        if (gp == p) return p;
+        atomicMin(lp + x, gp);
+        x = gp;
+    }
+}
+
+__device__ void lunion(uint32_t* lp, uint32_t a, uint32_t b)
+{
+    for (;;) {
+        a = lfind(lp, a);
+        b = lfind(lp, b);
+        if (a == b) return;
+        if (a < b) { uint32_t t = a; a = b; b = t; }
+        uint32_t old = atomicMin(lp + a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+// Overlapping runs / gaps of rows y and y+1 -> union (callback gets local or global ids).
+template <typename FG, typename BG>
+__device__ __forceinline__ void row_pair_unions(const RowGeom& g, const uint16_t* rs0, const uint16_t* re0, int n0,
+                                                const uint16_t* rs1, const uint16_t* re1, int n1, FG fg, BG bg)
+{
+    const int lane = threadIdx.x & 63;
+    // foreground, 8-connectivity: [a,b] ~ [c,d] iff c <= b+1 && d >= a-1
+    for (int i = lane; i < n0; i += 64) {
+        const int a = rs0[i], b = re0[i];
+        for (int j = lower_bound(re1, n1, a - 1); j < n1 && (int)rs1[j] <= b + 1; ++j) fg(i, j);
+    }
+    // background, 4-connectivity between non-empty gaps
+    for (int i = lane; i <= n0; i += 64) {
+        const int ga = i == 0 ? 0 : (int)re0[i - 1] + 1;
+        const int gb = i == n0 ? g.W - 1 : (int)rs0[i] - 1;
+        if (ga > gb) continue;
+        for (int j = lower_bound(rs1, n1, ga + 1); j <= n1; ++j) {  // first gap whose end >= ga
+            const int ca = j == 0 ? 0 : (int)re1[j - 1] + 1;
+            if (ca > gb) break;
+            const int cb = j == n1 ? g.W - 1 : (int)rs1[j] - 1;
+            if (ca <= cb) bg(i, j);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_band(const uint64_t* __restrict__ mbits, RowGeom g, int BH,
+                                               uint16_t* __restrict__ rs, uint16_t* __restrict__ re,
+                                               uint32_t* __restrict__ nfg, uint32_t* __restrict__ fpar,
+                                               uint32_t* __restrict__ gpar, uint32_t* __restrict__ area2,
+                                               unsigned long long* __restrict__ stats)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lp[];
+    __shared__ int s_n[32];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int y0 = blockIdx.x * BH, y = y0 + wave;
+    const bool act = y < g.H;
+    const uint32_t CAP = (uint32_t)g.CAP, FG0 = 1, GP0 = 1 + (uint32_t)BH * CAP;
+    const uint32_t base = (uint32_t)y * CAP;
+
+    // ---- phase 1: runs of row y (bit tricks + wave scan), written to global
+    int n = 0;
+    bool left_bg = true, right_bg = true;
+    unsigned long long motion = 0;
+    if (act) {
+        const uint64_t* row = mbits + (size_t)y * g.WW;
+        int ne = 0;
+        for (int b0 = 0; b0 < g.WW; b0 += 64) {
+            const int i = b0 + lane;
+            uint64_t w = 0, pw = 0, nw = 0;
+            if (i < g.WW) {
+                w = row[i];
+                pw = i > 0 ? row[i - 1] : 0;
+                nw = i + 1 < g.WW ? row[i + 1] : 0;
+            }
+            uint64_t st = w & ~((w << 1) | (pw >> 63));
+            uint64_t en = w & ~((w >> 1) | (nw << 63));
+            const int cs = __popcll(st), ce = __popcll(en);
+            const int ps = wave_incl_scan(cs), pe = wave_incl_scan(ce);
+            int ks = n + ps - cs, ke = ne + pe - ce;
+            while (st) { rs[base + ks++] = (uint16_t)(i * 64 + __ffsll((unsigned long long)st) - 1); st &= st - 1; }
+            while (en) { re[base + ke++] = (uint16_t)(i * 64 + __ffsll((unsigned long long)en) - 1); en &= en - 1; }
+            n += __shfl(ps, 63, 64);
+            ne += __shfl(pe, 63, 64);
+            motion += (unsigned long long)__popcll(w);
+        }
+        left_bg = !(row[0] & 1ull);
+        right_bg = !((row[(g.W - 1) >> 6] >> ((g.W - 1) & 63)) & 1ull);
+        for (int k = lane; k < n; k += 64) lp[FG0 + wave * CAP + k] = FG0 + wave * CAP + k;
+        for (int k = lane; k <= n; k += 64) {
+            const bool nonempty = (k == 0) ? left_bg : (k == n ? right_bg : true);
+            const bool border = y == 0 || y == g.H - 1 || k == 0 || k == n;
+            const uint32_t id = GP0 + wave * (CAP + 1) + k;
+            lp[id] = (nonempty && border) ? 0u : id;
+        }
+        if (lane == 0) s_n[wave] = n;
+    }
+    if (threadIdx.x == 0) lp[0] = 0;
+    for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);
+    if (lane == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
+    __syncthreads();
+
+    // ---- phase 2: unions between the band's consecutive rows, in LDS
+    if (act && wave + 1 < BH && y + 1 < g.H) {
+        const int n1 = s_n[wave + 1];
+        const uint32_t f0 = FG0 + wave * CAP, f1 = f0 + CAP;
+        const uint32_t q0 = GP0 + wave * (CAP + 1), q1 = q0 + CAP + 1;
+        row_pair_unions(g, rs + base, re + base, n, rs + base + CAP, re + base + CAP, n1,
+                        [&](int i, int j) { lunion(lp, f0 + i, f1 + j); },
+                        [&](int i, int j) { lunion(lp, q0 + i, q1 + j); });
+    }
+    __syncthreads();
+
+    // ---- phase 3: flatten; publish band-local roots as global ids (root = min id)
+    if (act) {
+        for (int k = lane; k < n; k += 64) {
+            const uint32_t r = lfind(lp, FG0 + wave * CAP + k) - FG0;
+            fpar[base + k] = (uint32_t)(y0 + r / CAP) * CAP + r % CAP;
+            area2[base + k] = 0;
+        }
+        const uint32_t gbase = 1u + (uint32_t)y * (CAP + 1);
+        for (int k = lane; k <= n; k += 64) {
+            const uint32_t r = lfind(lp, GP0 + wave * (CAP + 1) + k);
+            uint32_t gid;
+            if (r == 0) gid = 0;
+            else {
+                const uint32_t rr = r - GP0;
+                gid = 1u + (uint32_t)(y0 + rr / (CAP + 1)) * (CAP + 1) + rr % (CAP + 1);
+            }
+            gpar[gbase + k] = gid;
+        }
+        if (lane == 0) nfg[y] = (uint32_t)n;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
+}
+
+// ------------------------------------------------------------------ merge ---
+// One wave per band seam (rows b*BH-1 and b*BH): global unions of the band
+// roots, with monotone atomicMin links (uf_union).
+__global__ void __launch_bounds__(64) k_merge(RowGeom g, int BH, const uint16_t* __restrict__ rs,
                                               const uint16_t* __restrict__ re, const uint32_t* __restrict__ nfg,
                                               uint32_t* fpar, uint32_t* gpar)
 {
-    extern __shared__ __attribute__((aligned(16))) uint16_t s_u[];
-    const int y = blockIdx.x, lane = threadIdx.x;
-    const int n0 = (int)nfg[y], n1 = (int)nfg[y + 1];
-    uint16_t *rs0 = s_u, *re0 = s_u + g.CAP, *rs1 = s_u + 2 * g.CAP, *re1 = s_u + 3 * g.CAP;
+    const int y = (blockIdx.x + 1) * BH - 1;
+    if (y + 1 >= g.H) return;
     const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
-    for (int k = lane; k < n0; k += 64) { rs0[k] = rs[b0 + k]; re0[k] = re[b0 + k]; }
-    for (int k = lane; k < n1; k += 64) { rs1[k] = rs[b1 + k]; re1[k] = re[b1 + k]; }
-    __syncthreads();
-    // foreground: 8-connectivity, runs [a,b] and [c,d] touch iff c <= b+1 && d >= a-1
-    for (int i = lane; i < n0; i += 64) {
-        int a = rs0[i], b = re0[i];
-        for (int j = lower_bound(re1, n1, a - 1); j < n1 && (int)rs1[j] <= b + 1; ++j)
-            uf_union(fpar, b0 + i, b1 + j);
-    }
-    // background: 4-connectivity between non-empty gaps
     const uint32_t g0 = 1u + (uint32_t)y * (g.CAP + 1), g1 = g0 + (g.CAP + 1);
-    for (int i = lane; i <= n0; i += 64) {
-        int ga = i == 0 ? 0 : (int)re0[i - 1] + 1;
-        int gb = i == n0 ? g.W - 1 : (int)rs0[i] - 1;
-        if (ga > gb) continue;
-        // first gap j of row y+1 whose end >= ga: end_j = rs1[j]-1 (j<n1), W-1 (j==n1)
-        for (int j = lower_bound(rs1, n1, ga + 1); j <= n1; ++j) {
-            int ca = j == 0 ? 0 : (int)re1[j - 1] + 1;
-            if (ca > gb) break;
-            int cb = j == n1 ? g.W - 1 : (int)rs1[j] - 1;
-            if (ca <= cb) uf_union(gpar, g0 + i, g1 + j);
-        }
+    row_pair_unions(g, rs + b0, re + b0, (int)nfg[y], rs + b1, re + b1, (int)nfg[y + 1],
+                    [&](int i, int j) { uf_union(fpar, b0 + i, b1 + j); },
+                    [&](int i, int j) { uf_union(gpar, g0 + i, g1 + j); });
+}
+
+// ------------------------------------------------------------------ paint ---
+// One wave per row: the kept (filtered) mask, fd:101-104 — every run of a kept
+// component plus the holes between its runs (drawContours FILLED).
+__global__ void __launch_bounds__(64) k_paint(RowGeom g, const uint16_t* __restrict__ rs,
+                                              const uint16_t* __restrict__ re, const uint32_t* __restrict__ nfg,
+                                              const uint32_t* __restrict__ fpar, const uint8_t* __restrict__ gE,
+                                              const uint32_t* __restrict__ area2, int64_t min_area2,
+                                              uint64_t* __restrict__ kbits)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_k[];
+    const int y = blockIdx.x, lane = threadIdx.x;
+    for (int w = lane; w < g.WW; w += 64) s_k[w] = 0ull;
+    __syncthreads();
+    const int n = (int)nfg[y];
+    const uint32_t base = (uint32_t)y * g.CAP;
+    const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
+    for (int k = lane; k < n; k += 64) {
+        const uint32_t root = fpar[base + k];
+        if (!((int64_t)area2[root] > min_area2)) continue;  // contourArea > min_area
+        const int e = re[base + k];
+        paint_bits(s_k, 0, g.WW, rs[base + k], e);
+        if (k + 1 < n && !ge[k + 1]) paint_bits(s_k, 0, g.WW, e + 1, (int)rs[base + k + 1] - 1);
     }
+    __syncthreads();
+    for (int w = lane; w < g.WW; w += 64) kbits[(size_t)y * g.WW + w] = s_k[w];
 }
 
 // ---------------------------------------------------------------- resolve ---
@@ -415,7 +564,7 @@ __global__ void __launch_bounds__(64) k_area(RowGeom g, const uint16_t* __restri
         if (c) atomicAdd(area2 + r, (uint32_t)c);
     }
     for (int d = 32; d >= 1; d >>= 1) comps += __shfl_xor(comps, d, 64);
-    if (lane == 0 && comps) atomicAdd(stats + 2, (unsigned long long)comps);
+    if (lane == 0 && comps) atomicAdd(stats + STAT_SLOT(y) * 4 + 2, (unsigned long long)comps);
 }
 
 // ------------------------------------------------------------------- back ---
@@ -482,30 +631,29 @@ __global__ void __launch_bounds__(256) k_back(BackArgs a)
     const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
     const int k = a.ksize, an = a.anchor, NR = TH + k - 1;
     const int wx0 = (x0 >> 6) - 1;
-    const int xlo = wx0 * 64 < 0 ? 0 : wx0 * 64;
-    const int xhi = min((wx0 + NWD) * 64 - 1, a.g.W - 1);
 
-    for (int i = tid; i < NR * NWD; i += 256) s_k[i / NWD][i % NWD] = 0ull;
-    __syncthreads();
-    // paint kept runs (+ the holes between runs of a kept component)
-    for (int r = wave; r < NR; r += 4) {
-        int gy = y0 - an + r;
-        if (gy < 0 || gy >= a.g.H) continue;
-        const int n = (int)a.nfg[gy];
-        const uint32_t base = (uint32_t)gy * a.g.CAP;
-        const uint16_t* rrs = a.rs + base;
-        const uint16_t* rre = a.re + base;
-        const uint8_t* ge = a.gE + (size_t)gy * (a.g.CAP + 1);
-        int lo = lower_bound(rre, n, xlo);
-        int j0 = lo > 0 ? lo - 1 : 0;
-        for (int j = j0 + lane; j < n; j += 64) {
-            int s = rrs[j], e = rre[j];
-            if (s > xhi) break;
-            uint32_t root = a.fpar[base + j];
-            if (!((int64_t)a.area2[root] > a.min_area2)) continue;  // contourArea > min_area
-            if (e >= xlo) paint_bits(&s_k[r][0], wx0, NWD, s, e);
-            if (j + 1 < n && !ge[j + 1]) paint_bits(&s_k[r][0], wx0, NWD, e + 1, (int)rrs[j + 1] - 1);
+    // this lane's BxB block of BGR and accumulated mask: issued first, so the HBM
+    // latency hides under the kept-mask/dilation phases below
+    const int bx = x0 + lane * B, by = y0 + wave * B;
+    const bool active = bx < a.g.W && by < a.g.H;
+    uint32_t px[B][3 * B / 4];   // BGR, B px per row = 3B/4 dwords
+    uint32_t acv[B][B / 4];
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.bgr + (size_t)(by + i) * a.pitch + 3 * bx);
+#pragma unroll
+            for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
+            const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(by + i) * a.g.W + bx);
+#pragma unroll
+            for (int d = 0; d < B / 4; ++d) acv[i][d] = ac[d];
         }
+    }
+
+    // kept-mask window (k_paint): rows outside the image and words outside the row are 0
+    for (int i = tid; i < NR * NWD; i += 256) {
+        const int r = i / NWD, c = i % NWD, gy = y0 - an + r, gw = wx0 + c;
+        s_k[r][c] = (gy >= 0 && gy < a.g.H && gw >= 0 && gw < a.g.WW) ? a.kbits[(size_t)gy * a.g.WW + gw] : 0ull;
     }
     __syncthreads();
     // horizontal dilation: out bit x = OR src bits x-an .. x+k-1-an
@@ -528,35 +676,25 @@ __global__ void __launch_bounds__(256) k_back(BackArgs a)
         s_v[rr][c] = o;
     }
     __syncthreads();
-    if (a.dbg_kept || a.dbg_dil) {
+    if (a.dbg_dil) {
         for (int i = tid; i < TH * B; i += 256) {
             int rr = i / B, c = i % B, gy = y0 + rr, gw = (x0 >> 6) + c;
-            if (gy >= a.g.H || gw >= a.g.WW) continue;
-            if (a.dbg_kept) a.dbg_kept[(size_t)gy * a.g.WW + gw] = s_k[rr + an][c + 1];
-            if (a.dbg_dil) a.dbg_dil[(size_t)gy * a.g.WW + gw] = s_v[rr][c];
+            if (gy < a.g.H && gw < a.g.WW) a.dbg_dil[(size_t)gy * a.g.WW + gw] = s_v[rr][c];
         }
     }
 
     // per-block work: wave -> block row, lane -> block
-    const int bx = x0 + lane * B, by = y0 + wave * B;
-    bool active = bx < a.g.W && by < a.g.H;
     bool is_static = false;
     if (active) {
         const int W = a.g.W;
         uint32_t accn[B][B / 4];
-        uint32_t px[B][3 * B / 4];        // BGR, B px per row = 3B/4 dwords
         bool zero = true;
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            const int yy = by + i;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.bgr + (size_t)yy * a.pitch + 3 * bx);
-#pragma unroll
-            for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
-            const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)yy * W + bx);
             uint64_t dw = s_v[wave * B + i][(lane * B) >> 6] >> ((lane * B) & 63);
 #pragma unroll
             for (int d = 0; d < B / 4; ++d) {
-                uint32_t av = ac[d], nv = 0;
+                uint32_t av = acv[i][d], nv = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float dil = (float)(((dw >> (4 * d + j)) & 1ull) ? 255 : 0);
@@ -649,7 +787,8 @@ __global__ void __launch_bounds__(256) k_back(BackArgs a)
         }
     }
     unsigned long long bal = __ballot(active && is_static);
-    if (lane == 0 && bal) atomicAdd(a.stats + 3, (unsigned long long)__popcll(bal));
+    if (lane == 0 && bal)
+        atomicAdd(a.stats + STAT_SLOT(blockIdx.x * 4 + blockIdx.y * 7 + wave) * 4 + 3, (unsigned long long)__popcll(bal));
 }
 
 // --------------------------------------------------------------- launchers --
@@ -671,16 +810,27 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, const uint8_t* prev, uint
     return hipGetLastError();
 }
 
-hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, hipStream_t s)
+// Rows per band: the band's local parents (BH x (2 CAP + 1) u32) must fit LDS.
+int band_rows(const RowGeom& g)
 {
-    hipLaunchKernelGGL(k_runs, dim3(g.H), dim3(64), 4 * g.CAP, s, c.mbits, g, c.rs, c.re, c.nfg, c.fpar,
-                       c.gpar, c.area2, c.stats);
-    if (g.H > 1)
-        hipLaunchKernelGGL(k_union, dim3(g.H - 1), dim3(64), 8 * g.CAP, s, g, c.rs, c.re, c.nfg, c.fpar, c.gpar);
+    int bh = 16;
+    while (bh > 1 && (size_t)bh * (2 * g.CAP + 1) * 4 + 16 > 128 * 1024) bh >>= 1;
+    return bh;
+}
+
+hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int64_t min_area2, hipStream_t s)
+{
+    const int BH = band_rows(g), nb = (g.H + BH - 1) / BH;
+    const size_t lds = ((size_t)BH * (2 * g.CAP + 1) + 1) * 4;
+    hipLaunchKernelGGL(k_band, dim3(nb), dim3(64 * BH), lds, s, c.mbits, g, BH, c.rs, c.re, c.nfg, c.fpar, c.gpar,
+                       c.area2, c.stats);
+    if (nb > 1) hipLaunchKernelGGL(k_merge, dim3(nb - 1), dim3(64), 0, s, g, BH, c.rs, c.re, c.nfg, c.fpar, c.gpar);
     hipLaunchKernelGGL(k_resolve, dim3(g.H), dim3(64), 8 * g.WW + 4 * g.CAP + 16, s, g, c.rs, c.re, c.nfg,
                        c.fpar, c.gpar, c.gE, c.mbits, c.fbits);
     hipLaunchKernelGGL(k_area, dim3(g.H), dim3(64), 8 * g.WW, s, g, c.rs, c.re, c.nfg, c.fpar, c.gE, c.fbits,
                        c.area2, c.stats);
+    hipLaunchKernelGGL(k_paint, dim3(g.H), dim3(64), 8 * g.WW, s, g, c.rs, c.re, c.nfg, c.fpar, c.gE, c.area2,
+                       min_area2, c.kbits);
     return hipGetLastError();
 }
 

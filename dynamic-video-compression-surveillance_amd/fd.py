@@ -57,10 +57,15 @@ def _addr(x) -> int:
 
 class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
-                 device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False, **kwargs):
+                 device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
+                 pipeline: int = 1, **kwargs):
+        """``pipeline`` > 1 (device mode only) keeps that many frames in flight:
+        the contour filter of consecutive frames runs concurrently on internal
+        HIP streams while the front and back chains stay in frame order."""
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
             | (N.DVC_FLAG_KTIMING if ktiming else 0)
         self.params = derive_params(width, height, flags=flags, **kwargs)
+        self.params.pipeline = int(pipeline)
         self.W, self.H = int(width), int(height)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()

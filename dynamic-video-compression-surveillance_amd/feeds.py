@@ -1,0 +1,65 @@
+"""Independent camera feeds sharded one per GPU.
+
+The reference processes videos one after another on one worker thread
+(``windows.py:142-158``). Feeds are independent — within a feed frames are
+sequential through ``prev_gray``/``accumulated_mask`` (``fd:107,133``), so the
+feed is the parallel unit: one process per GPU (torchrun), each process owns
+the feeds ``feeds[rank::world]`` with no per-frame communication. The only
+collective is an end-of-run all-reduce of a few counters (RCCL on GPUs, gloo on
+CPU), plus the max-over-ranks wall time.
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, Sequence
+
+STAT_KEYS = ("frames", "motion_px", "components", "static_blocks")
+
+
+def dist_env():
+    """(rank, world, local_rank) from the torchrun environment (1 process if unset)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def shard(items: Sequence, rank: int, world: int) -> list:
+    """Round-robin shard: rank r owns items r, r+world, ... (weak scaling by feed)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of {world}")
+    return list(items[rank::world])
+
+
+def aggregate(stats: dict, elapsed_s: float | None = None, device=None) -> dict:
+    """Sum the per-rank counters and max the wall time over all ranks.
+
+    One all-reduce of a <= 64-byte vector at the end of a run (latency-bound over
+    xGMI); identity when torch.distributed is not initialised.
+    """
+    import torch
+    import torch.distributed as dist
+    vals = [float(stats.get(k, 0)) for k in STAT_KEYS]
+    vec = torch.tensor(vals, dtype=torch.float64, device=device)
+    t = torch.tensor([float(elapsed_s or 0.0)], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {k: int(round(v)) for k, v in zip(STAT_KEYS, vec.tolist())}
+    if elapsed_s is not None:
+        out["elapsed_max_s"] = float(t.item())
+    return out
+
+
+def process_feeds(video_paths: Iterable[str], output_dir: str, technique: str = "Frame Differencing",
+                  **kwargs) -> list:
+    """Run this rank's shard of ``video_paths`` through the reference-compatible
+    driver (windows.py:144-158 picks the technique by its combo-box label).
+    Returns the paths this rank processed."""
+    rank, world, local = dist_env()
+    os.environ.setdefault("DVC_DEVICE", str(local))
+    mine = shard(list(video_paths), rank, world)
+    if technique != "Frame Differencing":
+        raise NotImplementedError(f"technique {technique!r}: only the frame-differencing path is accelerated")
+    from .frame_differencing import process_single_video_fd
+    for p in mine:
+        process_single_video_fd(p, output_dir, **kwargs)
+    return mine

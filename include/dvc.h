@@ -71,6 +71,7 @@ extern "C" {
  *                 1-release_factor, 0 (fd:107).
  *   quant         quantization_level as float32 (fd:123).
  *   prime_ksize,prime_sigma  GaussianBlur of frame 0: 25, 30.0 (fd:77).
+ *   pipeline      frames in flight (see the field).
  */
 typedef struct dvc_fd_params {
     int32_t width;
@@ -87,7 +88,10 @@ typedef struct dvc_fd_params {
     int32_t prime_ksize;
     double prime_sigma;
     uint32_t flags;
-    uint32_t reserved;
+    uint32_t pipeline;  /* frames in flight: 0/1 = every launch in order on the
+                           handle's stream; 2..8 (DVC_FLAG_DEVICE_PTRS only) = the
+                           contour filter of consecutive frames overlapped on
+                           internal streams (front and back chains stay ordered) */
 } dvc_fd_params;
 
 /* Cumulative per-handle counters (all frames stepped since create/prime). */

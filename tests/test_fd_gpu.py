@@ -169,6 +169,37 @@ def test_graph_replay_matches_eager(gpu_lib):
     assert outs[0][2] == outs[1][2]
 
 
+@pytest.mark.parametrize("depth", [2, 3])
+def test_pipelined_matches_sequential(gpu_lib, depth):
+    """Frames in flight on internal streams (eager and hipGraph) == in-order launches."""
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = torch.from_numpy(clip(640, 360, 8, seed=6, noisy=True)).to("cuda:0")
+    order = [1, 2, 3, 4, 5, 6, 7, 6, 5, 4, 3, 2]       # 12 steps: multiple of 2 and of depth
+    outs = []
+    for mode in ("seq", "pipe", "pipe_graph"):
+        ov = torch.empty((len(order), 360, 640, 3), dtype=torch.uint8, device="cuda:0")
+        cp = torch.empty_like(ov)
+        w = gpu_lib.FDWorker(640, 360, device_ptrs=True, pipeline=1 if mode == "seq" else depth)
+        w.prime(frames[0])
+        for rep in range(2):
+            if mode == "pipe_graph" and rep == 0:
+                w.graph_begin()
+            if mode == "pipe_graph" and rep == 1:
+                w.graph_end()
+                w.graph_launch()
+                w.graph_launch()
+                break
+            for j, t in enumerate(order):
+                w.step(frames[t], ov[j], cp[j])
+        w.sync()
+        outs.append((ov.cpu().numpy(), cp.cpu().numpy(), w.stats()))
+        w.close()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
+        assert outs[0][2] == o[2]
+
+
 def test_errors(gpu_lib):
     from dvc_amd._native import DvcError
     with pytest.raises(DvcError):

@@ -1,0 +1,140 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol
+include/dvc.h declares (no compute calls), parameter derivation, the reference's
+execution_times.txt format, frame I/O, the synthetic generator, feed sharding."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "dvc.h")).read()
+    return sorted(set(re.findall(r"\b(dvc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_abi_exports_every_declared_symbol():
+    import dvc_amd
+    dvc_amd._native.build()
+    L = dvc_amd._native.lib()
+    declared = _declared_symbols()
+    assert set(declared) == set(dvc_amd._native.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.dvc_abi_version() == 1
+
+
+def test_abi_gaussian_taps_host_only():
+    """dvc_gaussian_taps_q8 is pure host code: same taps as the oracle."""
+    import dvc_amd
+    import oracle
+    for n, s in [(5, 0.0), (25, 30.0), (7, 1.2), (31, 5.0)]:
+        assert dvc_amd._native.gaussian_taps_q8(n, s) == oracle.gauss_taps_q8(n, s).tolist()
+
+
+def test_derive_params_matches_reference_semantics():
+    from dvc_amd.fd import derive_params
+    p = derive_params(1920, 1080)
+    assert (p.block, p.ithresh, p.min_area2, p.ksize, p.anchor) == (4, 0, 1000, 7, 3)
+    assert (p.alpha, p.beta, p.gamma, p.quant) == (0.5, 0.5, 0.0, 100.0)
+    assert (p.prime_ksize, p.prime_sigma) == (25, 30.0)
+    # fd:200-207 variant and edge thresholds
+    p = derive_params(960, 540, block_size=8, kernel_size=10, release_factor=0.3, min_area=10.25,
+                      motion_threshold=-3)
+    assert (p.block, p.ksize, p.anchor, p.min_area2, p.ithresh) == (8, 10, 5, 20, -1)
+    assert p.alpha == np.float32(0.3) and p.beta == np.float32(1 - 0.3)
+    assert derive_params(16, 16, motion_threshold=999).ithresh == 255
+
+
+def test_execution_times_format(tmp_path):
+    """Parsed with the reference's own rules (performance_analysis.py:42-107, restated)."""
+    from dvc_amd.frame_differencing import write_execution_times
+    p = tmp_path / "execution_times.txt"
+    write_execution_times(p, 99, 12.3456, 0.12345)
+    lines = [ln.strip() for ln in open(p) if ln.strip()]
+    assert lines[0] == "Frame Differencing:"
+    pat = r":\s*([\d\.]+)"
+    assert int(re.search(pat, lines[1]).group(1)) == 99
+    assert float(re.search(pat, lines[2]).group(1)) == 12.35
+    assert float(re.search(pat, lines[3]).group(1)) == 0.1235
+    assert lines[4] == "Total video processing time: 12.35 seconds"
+
+
+def test_npy_stream_writer_and_source(tmp_path):
+    from dvc_amd import video_io
+    frames = np.random.default_rng(0).integers(0, 256, (5, 24, 32, 3), dtype=np.uint8)
+    w = video_io.open_sink(str(tmp_path / "out.mp4"), 25, (32, 24))
+    for f in frames:
+        w.write(f)
+    w.write(np.zeros((10, 10, 3), np.uint8))   # wrong size: dropped like cv2.VideoWriter
+    w.release()
+    back = np.load(tmp_path / "out.npy")
+    assert np.array_equal(back, frames)
+    cap = video_io.open_source(str(tmp_path / "out.npy"))
+    assert cap.isOpened() and cap.get(video_io.CAP_PROP_FPS) == 25.0
+    assert cap.get(video_io.CAP_PROP_FRAME_WIDTH) == 32
+    got = []
+    while True:
+        ok, f = cap.read()
+        if not ok:
+            break
+        got.append(f)
+    assert np.array_equal(np.stack(got), frames)
+    assert not video_io.open_source(str(tmp_path / "missing.npy")).isOpened()
+
+
+def test_synthetic_deterministic_and_moving():
+    from dvc_amd.synthetic import SyntheticClip, background, clip
+    a = clip(160, 96, 4, seed=3)
+    b = clip(160, 96, 4, seed=3)
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a[0], a[1])
+    bg = background(8, 4)
+    assert bg[0, 0].tolist() == [28, 28 + 29, 28 + 58]
+    c = SyntheticClip(640, 360, seed=0, noisy=True)
+    assert len(c.objects) == 6
+    d = c.frame(1).astype(int) - SyntheticClip(640, 360, seed=0).frame(1).astype(int)
+    assert 0 < (d != 0).any(-1).mean() < 0.01 and np.abs(d).max() <= 3
+
+
+def test_resize_frame_semantics():
+    from dvc_amd.frame_differencing import resize_frame
+    f = np.random.default_rng(1).integers(0, 256, (8, 10, 3), dtype=np.uint8)
+    assert resize_frame(f, (10, 8)) is f
+    h = resize_frame(f, (5, 4))
+    exp = (f[0::2, 0::2].astype(int) + f[0::2, 1::2] + f[1::2, 0::2] + f[1::2, 1::2] + 2) >> 2
+    assert np.array_equal(h, exp)
+    with pytest.raises(NotImplementedError):
+        resize_frame(f, (7, 5))
+
+
+def test_video_name():
+    from dvc_amd.video_io import video_name
+    assert video_name("/a/b/cam01.mp4") == "cam01"
+    assert video_name("synthetic://640x360?frames=5") == "640x360"
+
+
+def test_unopenable_video_logs_and_returns(tmp_path, caplog):
+    from dvc_amd.frame_differencing import filter_and_dilate_movements
+    with caplog.at_level("ERROR"):
+        assert filter_and_dilate_movements(str(tmp_path / "nope.npy"), str(tmp_path)) is None
+    assert "Unable to open the video." in caplog.text
+
+
+def test_shard():
+    from dvc_amd.feeds import shard
+    feeds = [f"cam{i}" for i in range(10)]
+    parts = [shard(feeds, r, 4) for r in range(4)]
+    assert sorted(sum(parts, [])) == sorted(feeds)
+    assert parts[1] == ["cam1", "cam5", "cam9"]
+    with pytest.raises(ValueError):
+        shard(feeds, 4, 4)
+
+
+def test_pingpong_order():
+    import bench
+    o = bench.pingpong(64)
+    assert len(o) == 126 and o[0] == 0 and o[63] == 63 and o[-1] == 1
+    assert all(abs(a - b) == 1 for a, b in zip(o, o[1:] + o[:1]))
