@@ -7,11 +7,13 @@ Workload (BASELINE.json configs[1]): one synthetic 1920x1080 camera feed per
 GPU (seed = rank), the full per-frame worker of frame_differencing.py:91-133 —
 gray, 5x5 blur, absdiff/threshold, contour-area filter, 7x7 dilate,
 accumulation, red overlay, static-block DCT quantisation, YCrCb round trip —
-with the GUI's default kwargs (windows.py:154). Frames are device-resident: a
-ring of 64 distinct frames (398 MB, beyond the 256 MB Infinity Cache) played
-ping-pong (0..63..1) so every consecutive pair is real motion; overlay and
-compressed outputs go to 126-slot device rings. A step = one 126-frame pass,
-captured once as a hipGraph and replayed.
+with the GUI's default kwargs (windows.py:154). Frames are device-resident: 64
+distinct synthetic frames played ping-pong (0..63..1) so every consecutive pair
+is real motion, materialised as one contiguous 126-frame sequence (784 MB,
+beyond the 256 MB Infinity Cache); overlay and compressed outputs go to
+126-frame device buffers. A step = one pass over the 126 frames through
+dvc_fd_step_batch (launches of --batch frames; --per-frame: one dvc_fd_step
+per frame instead).
 
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
@@ -34,7 +36,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/s (frames/s × H×W) 1080p frame-diff path @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BACK_BYTES_PER_PX = 11         # k_back algorithmic: read BGR 3 + acc 1; write acc 1 + overlay 3 + compressed 3
+# k_back algorithmic bytes: per frame read BGR 3 + kept-mask 1/8, write overlay 3 + compressed 3;
+# per launch (batch) read + write the accumulated mask once (1 + 1)
+BACK_BYTES_PER_PX_FRAME = 9.125
+BACK_BYTES_PER_PX_LAUNCH = 2
 PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 read, new gray 1 written
 
 
@@ -85,10 +90,8 @@ def main():
     ap.add_argument("--noisy", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="launch per frame instead of replaying a hipGraph")
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="frames in flight (contour filter of consecutive frames on concurrent HIP streams); "
-                         "must divide the 126-frame step")
+    ap.add_argument("--batch", type=int, default=63, help="frames per device launch (max_batch)")
+    ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
     args = ap.parse_args()
 
     import numpy as np
@@ -108,35 +111,36 @@ def main():
 
     W, H, R = args.width, args.height, args.ring
     clip = SyntheticClip(W, H, seed=rank, noisy=args.noisy)
-    ring = torch.empty((R, H, W, 3), dtype=torch.uint8, device=dev)
-    for i in range(R):
-        ring[i].copy_(torch.from_numpy(clip.frame(i)))
     order = pingpong(R)
-    P = len(order)                 # frames per step (126 for R=64), even
-    ov = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
-    cp = torch.empty_like(ov)
+    P = len(order)                 # frames per step (126 for R=64)
+    # frame j of a step is ring frame order[(j + 1) % P] (frame 0 primes the feed)
+    seq = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
+    for i in range(R):
+        f = torch.from_numpy(clip.frame(i)).to(dev)
+        for j in range(P):
+            if order[(j + 1) % P] == i:
+                seq[j].copy_(f)
+    first = torch.from_numpy(clip.frame(0)).to(dev)
+    ov = torch.empty_like(seq)
+    cp = torch.empty_like(seq)
     torch.cuda.synchronize()
+    batch = 1 if args.per_frame else max(1, min(args.batch, P))
 
     def make_worker(ktiming=False):
-        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming, pipeline=args.pipeline)
-        w.prime(ring[0])
+        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch)
+        w.prime(first)
         return w
 
-    def run_steps(w, n, graph):
+    def run_steps(w, n):
         for _ in range(n):
-            if graph:
-                w.graph_launch()
-            else:
+            if args.per_frame:
                 for j in range(P):
-                    w.step(ring[order[(j + 1) % P]], ov[j], cp[j])
+                    w.step(seq[j], ov[j], cp[j])
+            else:
+                w.step_batch(seq, ov, cp)
 
     w = make_worker()
-    graph = not args.eager
-    if graph:
-        w.graph_begin()
-        run_steps(w, 1, graph=False)
-        w.graph_end()
-    run_steps(w, args.warmup, graph)
+    run_steps(w, args.warmup)
     w.sync()
 
     def barrier():
@@ -146,7 +150,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    run_steps(w, args.steps, graph)
+    run_steps(w, args.steps)
     w.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -155,13 +159,15 @@ def main():
     st = w.stats()
     w.close()
 
-    # dominant kernel: hipEvent-timed k_back launches, same steps (eager: events need a plain stream)
+    # dominant kernel: hipEvent-timed k_back launches (on the back stream), same steps
     wk = make_worker(ktiming=True)
-    run_steps(wk, 1, graph=False)
+    run_steps(wk, 1)
     wk.ktime(reset=True)
-    run_steps(wk, max(1, min(args.steps, 10)), graph=False)
+    ksteps = max(1, min(args.steps, 10))
+    run_steps(wk, ksteps)
     kms, kn = wk.ktime()
     wk.close()
+    kframes = ksteps * P
 
     vec = torch.tensor([elapsed, st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
                        dtype=torch.float64, device=dev)
@@ -176,7 +182,8 @@ def main():
 
     if rank == 0:
         avg_ms = kms / max(kn, 1)
-        achieved = BACK_BYTES_PER_PX * W * H / (avg_ms * 1e-3) / 1e9
+        bytes_per_launch = (BACK_BYTES_PER_PX_FRAME * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_back")
         line = {
             "metric": METRIC,
@@ -193,15 +200,16 @@ def main():
             "data": "synthetic",
             "config": {"workload": "fd_1080p_single_feed_per_gpu" if (W, H) == (1920, 1080) else f"fd_{W}x{H}",
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": 1,
-                       "ring_frames": R, "noisy": args.noisy, "launch": "hipgraph" if graph else "eager",
-                       "frames_in_flight": args.pipeline,
+                       "ring_frames": R, "noisy": args.noisy,
+                       "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
                        "pipeline_bytes_per_px": PIPE_BYTES_PER_PX,
                        "pipeline_GBps_per_gpu": round(PIPE_BYTES_PER_PX * args.steps * P * W * H / elapsed_max / 1e9, 1)},
             "roofline": {"bound": "hbm", "kernel": "k_back", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": BACK_BYTES_PER_PX * W * H,
+                         "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         "frames_per_launch": round(kframes / max(kn, 1), 2),
                          "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn},
             "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
                       "static_blocks": int(vec[4])},

@@ -2,7 +2,8 @@
 
 The reference has no FFI: it calls ``cv2.*`` inside the per-frame loop of
 ``frame_differencing.py:85-138``. This module is the thin layer that replaces
-those calls with one ``dvc_fd_step`` per frame. There is deliberately no CPU
+those calls with one ``dvc_fd_step`` per frame (or one ``dvc_fd_step_batch``
+per run of frames). There is deliberately no CPU
 fallback: if the HIP library is missing or fails to load, :func:`lib` raises.
 """
 from __future__ import annotations
@@ -16,6 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
 SOURCES = ["fd_kernels.hip", "fd_api.hip"]
+HEADERS = ["fd_kernels.h", "dvc_device.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 DVC_OK = 0
@@ -29,9 +31,10 @@ PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
 EXPORTS = [
     "dvc_abi_version", "dvc_last_error", "dvc_device_count", "dvc_fd_create", "dvc_fd_prime",
     "dvc_fd_step", "dvc_fd_sync", "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime",
-    "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter",
-    "dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch",
+    "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter", "dvc_fd_step_batch",
 ]
+ABI_VERSION = 2
+MAX_BATCH = 512
 
 
 class DvcError(RuntimeError):
@@ -58,7 +61,7 @@ class FdParams(ctypes.Structure):
         ("prime_ksize", ctypes.c_int32),
         ("prime_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
-        ("pipeline", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
     ]
 
 
@@ -74,7 +77,7 @@ class FdStats(ctypes.Structure):
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile the HIP library in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, "fd_kernels.h"), os.path.join(PKG_DIR, "..", "include", "dvc.h")]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(PKG_DIR, "..", "include", "dvc.h")]
     if not force and os.path.exists(LIB_PATH):
         newest = max(os.path.getmtime(d) for d in deps if os.path.exists(d))
         if os.path.getmtime(LIB_PATH) >= newest:
@@ -124,15 +127,15 @@ def lib() -> ctypes.CDLL:
     L.dvc_fd_destroy.argtypes = [vp]
     L.dvc_fd_destroy.restype = None
     L.dvc_gaussian_taps_q8.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint16)]
-    for name in ("dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch"):
-        getattr(L, name).argtypes = [vp]
+    L.dvc_fd_step_batch.argtypes = [vp, u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u8p, u8p,
+                                    ctypes.c_size_t]
     L.dvc_contour_filter.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, u8p,
                                      ctypes.POINTER(ctypes.c_uint64)]
     for name in ("dvc_device_count", "dvc_fd_create", "dvc_fd_prime", "dvc_fd_step", "dvc_fd_sync",
                  "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime", "dvc_gaussian_taps_q8",
-                 "dvc_contour_filter", "dvc_fd_graph_begin", "dvc_fd_graph_end", "dvc_fd_graph_launch"):
+                 "dvc_contour_filter", "dvc_fd_step_batch"):
         getattr(L, name).restype = ctypes.c_int
-    if L.dvc_abi_version() != 1:
+    if L.dvc_abi_version() != ABI_VERSION:
         raise ImportError("libdvc_hip.so ABI version mismatch")
     _lib = L
     return L

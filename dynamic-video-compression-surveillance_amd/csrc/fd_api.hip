@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -92,89 +93,60 @@ void dct_matrix(int B, float* M)
 
 }  // namespace
 
-// Contour-filter scratch of one frame in flight.
+// Contour-filter scratch of one batch in flight (max_batch frames).
 struct Slot {
-    uint64_t *mbits = nullptr, *fbits = nullptr, *kbits = nullptr;
-    uint16_t *rs = nullptr, *re = nullptr;
-    uint32_t *nfg = nullptr, *fpar = nullptr, *gpar = nullptr, *area2 = nullptr;
-    uint8_t* gE = nullptr;
-    hipStream_t s_ccl = nullptr;
-    hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_back = nullptr;
-    bool recorded = false;  // ev_ccl / ev_back hold a frame that later frames must wait for
-    hipGraphNode_t node_ccl = nullptr, node_back = nullptr;  // graph building: last frame of this slot
+    dvc::CclBufs c{};
+    hipEvent_t ev_ccl = nullptr, ev_back = nullptr;
+    bool recorded = false;  // ev_back holds a batch that the next user of the slot must wait for
 };
-
-constexpr int MAX_DEPTH = 8;
 
 struct dvc_fd {
     dvc_fd_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;  // the caller's stream: prime, sequential mode, capture origin
+    hipStream_t stream = nullptr;  // front + contour filter (and prime); the caller's stream if given
     bool own_stream = false;
+    hipStream_t s_back = nullptr;  // back chain (accumulated mask), internal
     dvc::RowGeom g{};
     dvc::GaussTaps kprime{};
     dvc::DctMat M{};
     bool primed = false;
-    int cur = 0;                   // gray[cur] = previous blurred gray
-    uint64_t frames = 0;
-    // pipelining: `depth` frames in flight; front and back chains on their own
-    // streams, the contour filter of frame t on slot[t % depth].s_ccl
-    int depth = 1;
-    uint64_t seq = 0;
-    Slot slot[MAX_DEPTH];
-    hipStream_t s_front = nullptr, s_back = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join[2 + MAX_DEPTH] = {};
+    int max_batch = 1;
+    uint64_t frames = 0, seq = 0;  // frames stepped, batches launched
+    int last_n = 0;                // frames of the last batch
+    // Two slots: the front + contour filter of batch i+1 overlap the back of batch i.
+    Slot slot[2];
     // device state
-    uint8_t* gray[2] = {nullptr, nullptr};
-    uint8_t* acc = nullptr;
+    uint8_t* gray = nullptr;       // previous blurred gray (fd:77, 133)
+    uint8_t* acc = nullptr;        // accumulated mask (fd:81, 107)
     uint64_t* dbg_dil = nullptr;
     uint32_t* tmp32 = nullptr;
     uint8_t* gtmp = nullptr;
     unsigned long long* stats = nullptr;
-    // host-pointer staging
-    uint8_t *d_frame = nullptr, *d_ov = nullptr, *d_cp = nullptr;
+    // host-pointer staging (max_batch frames)
+    uint8_t *d_in = nullptr, *d_ov = nullptr, *d_cp = nullptr;
     uint8_t *h_in = nullptr, *h_ov = nullptr, *h_cp = nullptr, *h_acc = nullptr;
     // dominant-kernel timing
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
-    // hipGraph of a captured frame sequence
-    bool capturing = false;
-    int cap_cur = 0;
-    uint64_t cap_frames = 0, cap_seq = 0;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t gexec = nullptr;
-    bool eager_dirty = false;  // pipelined eager steps since the last graph launch
-    bool graph_dirty = false;  // a graph launch since the last pipelined eager step
-    hipStream_t cap_stream = nullptr;  // private stream the stages are captured on
-    hipGraphNode_t last_front = nullptr, last_back = nullptr;
 };
 
 static void free_all(dvc_fd* h)
 {
     for (Slot& s : h->slot) {
-        void* dev[] = {s.mbits, s.fbits, s.kbits, s.rs, s.re, s.nfg, s.fpar, s.gpar, s.area2, s.gE};
+        void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE};
         for (void* p : dev)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_back})
+        for (hipEvent_t e : {s.ev_ccl, s.ev_back})
             if (e) (void)hipEventDestroy(e);
-        if (s.s_ccl && s.s_ccl != h->stream) (void)hipStreamDestroy(s.s_ccl);
     }
-    void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_frame,
-                   h->d_ov, h->d_cp};
+    void* dev[] = {h->gray, h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     void* pin[] = {h->h_in, h->h_ov, h->h_cp, h->h_acc};
     for (void* p : pin)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    for (hipEvent_t e : h->ev_join)
-        if (e) (void)hipEventDestroy(e);
-    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-    if (h->graph) (void)hipGraphDestroy(h->graph);
-    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
-    if (h->s_front && h->s_front != h->stream) (void)hipStreamDestroy(h->s_front);
-    if (h->s_back && h->s_back != h->stream) (void)hipStreamDestroy(h->s_back);
+    if (h->s_back) (void)hipStreamDestroy(h->s_back);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
 }
 
@@ -184,28 +156,11 @@ static hipError_t dalloc(T** p, size_t bytes)
     return hipMalloc(reinterpret_cast<void**>(p), bytes ? bytes : 16);
 }
 
-// every stream the handle may have work on
-static int all_streams(dvc_fd* h, hipStream_t* out)
-{
-    int n = 0;
-    out[n++] = h->stream;
-    if (h->depth > 1) {
-        out[n++] = h->s_front;
-        out[n++] = h->s_back;
-        for (int i = 0; i < h->depth; ++i) out[n++] = h->slot[i].s_ccl;
-    }
-    return n;
-}
-
 static hipError_t sync_all(dvc_fd* h)
 {
-    hipStream_t s[2 + MAX_DEPTH];
-    int n = all_streams(h, s);
-    for (int i = 0; i < n; ++i) {
-        hipError_t e = hipStreamSynchronize(s[i]);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && h->s_back) e = hipStreamSynchronize(h->s_back);
+    return e;
 }
 
 extern "C" {
@@ -241,14 +196,12 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         return fail(DVC_E_INVALID, "dilation kernel %d (anchor %d) outside 1..63", p.ksize, p.anchor);
     if (p.ithresh < -1 || p.ithresh > 255) return fail(DVC_E_INVALID, "ithresh %d outside -1..255", p.ithresh);
     if (!(p.quant == p.quant) || p.quant == 0.0f) return fail(DVC_E_INVALID, "quantization_level must be nonzero");
-    const int depth = p.pipeline <= 1 ? 1 : (int)p.pipeline;
-    if (depth > MAX_DEPTH) return fail(DVC_E_INVALID, "pipeline depth %d outside 1..%d", depth, MAX_DEPTH);
-    if (depth > 1 && !(p.flags & DVC_FLAG_DEVICE_PTRS))
-        return fail(DVC_E_INVALID, "a pipeline depth > 1 needs DVC_FLAG_DEVICE_PTRS");
+    const int mb = p.max_batch == 0 ? 1 : (int)p.max_batch;
+    if (p.max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %u outside 1..%d", p.max_batch, DVC_MAX_BATCH);
     dvc_fd* h = new dvc_fd();
     h->p = p;
     h->device = device;
-    h->depth = depth;
+    h->max_batch = mb;
     h->g.W = p.width;
     h->g.H = p.height;
     h->g.WW = (p.width + 63) / 64;
@@ -274,238 +227,114 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if (e != hipSuccess) return bad(e, "hipStreamCreate");
         h->own_stream = true;
     }
-    const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW, CAP = h->g.CAP;
-    for (int i = 0; i < depth; ++i) {
-        Slot& s = h->slot[i];
-        struct { void** ptr; size_t bytes; } allocs[] = {
-            {(void**)&s.mbits, 8 * H * WW}, {(void**)&s.fbits, 8 * H * WW}, {(void**)&s.kbits, 8 * H * WW},
-            {(void**)&s.rs, 2 * H * CAP}, {(void**)&s.re, 2 * H * CAP}, {(void**)&s.nfg, 4 * H},
-            {(void**)&s.fpar, 4 * H * CAP}, {(void**)&s.gpar, 4 * (1 + H * (CAP + 1))},
-            {(void**)&s.gE, H * (CAP + 1)}, {(void**)&s.area2, 4 * H * CAP},
-        };
-        for (auto& a : allocs)
-            if ((e = dalloc(a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
-        if (depth > 1) {
-            if ((e = hipStreamCreateWithFlags(&s.s_ccl, hipStreamNonBlocking)) != hipSuccess)
-                return bad(e, "hipStreamCreate");
-            for (hipEvent_t* ev : {&s.ev_front, &s.ev_ccl, &s.ev_back})
-                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
-                    return bad(e, "hipEventCreate");
-        } else {
-            s.s_ccl = h->stream;
-        }
-    }
-    if (depth > 1) {
-        for (hipStream_t* st : {&h->s_front, &h->s_back})
-            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-        if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess)
-            return bad(e, "hipEventCreate");
-        for (hipEvent_t& ev : h->ev_join)
-            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-    } else {
-        h->s_front = h->s_back = h->stream;
+    if ((e = hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
+    for (Slot& s : h->slot) {
+        size_t sz[10];
+        dvc::CclBufs::sizes(h->g, mb, sz);
+        void** ptrs[10] = {(void**)&s.c.mbits, (void**)&s.c.fbits, (void**)&s.c.rs, (void**)&s.c.re,
+                           (void**)&s.c.nfg, (void**)&s.c.fpar, (void**)&s.c.gpar, (void**)&s.c.gE,
+                           (void**)&s.c.area2, (void**)&s.c.kbits};
+        for (int i = 0; i < 10; ++i)
+            if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
+        for (hipEvent_t* ev : {&s.ev_ccl, &s.ev_back})
+            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
     struct { void** ptr; size_t bytes; } allocs[] = {
-        {(void**)&h->gray[0], N}, {(void**)&h->gray[1], N}, {(void**)&h->acc, N}, {(void**)&h->stats, 8 * 4 * 64},
+        {(void**)&h->gray, N}, {(void**)&h->acc, N}, {(void**)&h->stats, 8 * 4 * 64},
     };
     for (auto& a : allocs)
         if ((e = dalloc(a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
+    for (Slot& s : h->slot) s.c.stats = h->stats;
     if (p.flags & DVC_FLAG_KEEP_PLANES) {
         if ((e = dalloc(&h->dbg_dil, 8 * H * WW)) != hipSuccess) return bad(e, "hipMalloc");
     }
     if (!(p.flags & DVC_FLAG_DEVICE_PTRS)) {
-        if ((e = dalloc(&h->d_frame, 3 * N)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&h->d_ov, 3 * N)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&h->d_cp, 3 * N)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_in, 3 * N)) != hipSuccess) return bad(e, "hipHostMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_ov, 3 * N)) != hipSuccess) return bad(e, "hipHostMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_cp, 3 * N)) != hipSuccess) return bad(e, "hipHostMalloc");
+        const size_t F = 3 * N * (size_t)mb;
+        if ((e = dalloc(&h->d_in, F)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = dalloc(&h->d_ov, F)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = dalloc(&h->d_cp, F)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_in, F)) != hipSuccess) return bad(e, "hipHostMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_ov, F)) != hipSuccess) return bad(e, "hipHostMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_cp, F)) != hipSuccess) return bad(e, "hipHostMalloc");
         if ((e = hipHostMalloc((void**)&h->h_acc, N)) != hipSuccess) return bad(e, "hipHostMalloc");
     }
     if ((e = hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return bad(e, "hipStreamSynchronize");
     *out = h;
-    return DVC_OK;
-}
-
-// Stage a host frame (any pitch) into the compact device frame buffer.
-static int stage_in(dvc_fd* h, const uint8_t* bgr, size_t pitch, const uint8_t** dptr, int* dpitch)
-{
-    const size_t W = h->p.width, H = h->p.height;
-    if (h->p.flags & DVC_FLAG_DEVICE_PTRS) {
-        *dptr = bgr;
-        *dpitch = (int)pitch;
-        return DVC_OK;
-    }
-    for (size_t y = 0; y < H; ++y) std::memcpy(h->h_in + y * 3 * W, bgr + y * pitch, 3 * W);
-    HIP_OK(hipMemcpyAsync(h->d_frame, h->h_in, 3 * W * H, hipMemcpyHostToDevice, h->stream));
-    *dptr = h->d_frame;
-    *dpitch = (int)(3 * W);
     return DVC_OK;
 }
 
 int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 {
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
-    if (h->capturing) return fail(DVC_E_STATE, "prime during graph capture");
     if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
-    const size_t N = (size_t)h->p.width * h->p.height;
+    const size_t W = h->p.width, H = h->p.height, N = W * H;
     if (!h->tmp32) {
         HIP_OK(dalloc(&h->tmp32, 4 * N));
         HIP_OK(dalloc(&h->gtmp, N));
     }
-    HIP_OK(sync_all(h));  // no frame of a previous run may still be in flight
-    const uint8_t* d;
-    int dp;
-    int rc = stage_in(h, bgr, pitch, &d, &dp);
-    if (rc) return rc;
-    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->cur], h->p.width, h->p.height, h->kprime,
-                             h->stream));
+    HIP_OK(sync_all(h));  // no batch of a previous run may still be in flight
+    const uint8_t* d = bgr;
+    int dp = (int)pitch;
+    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
+        for (size_t y = 0; y < H; ++y) std::memcpy(h->h_in + y * 3 * W, bgr + y * pitch, 3 * W);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, 3 * N, hipMemcpyHostToDevice, h->stream));
+        d = h->d_in;
+        dp = (int)(3 * W);
+    }
+    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray, h->p.width, h->p.height, h->kprime, h->stream));
     HIP_OK(hipMemsetAsync(h->acc, 0, N, h->stream));
     HIP_OK(hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream));
-    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS) || h->depth > 1) HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
     for (Slot& s : h->slot) s.recorded = false;
     h->frames = 0;
     h->seq = 0;
+    h->last_n = 0;
     h->primed = true;
     return DVC_OK;
 }
 
 }  // extern "C"
 
-// The three stages of one frame, each enqueued on one stream.
-static hipError_t stage_front(dvc_fd* h, Slot& S, const uint8_t* d, int dp, hipStream_t s)
+// Enqueue one batch of n <= max_batch device-resident frames:
+//   stream:  [wait back(i-2)] front(i) -> contour filter(i) -> ev_ccl
+//   s_back:  [wait ev_ccl] back(i) -> ev_back
+static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
+                         size_t ostride)
 {
-    return dvc::launch_front(d, dp, h->gray[h->cur], h->gray[h->cur ^ 1], S.mbits, h->g, h->p.ithresh, s);
-}
-
-static hipError_t stage_ccl(dvc_fd* h, Slot& S, hipStream_t s)
-{
-    dvc::CclBufs c{S.mbits, S.fbits, S.rs, S.re, S.nfg, S.fpar, S.gpar, S.gE, S.area2, S.kbits, h->stats};
-    return dvc::launch_ccl(c, h->g, h->p.min_area2, s);
-}
-
-static dvc::BackArgs back_args(dvc_fd* h, Slot& S, const uint8_t* d, int dp, uint8_t* ov, uint8_t* cp)
-{
+    Slot& S = h->slot[h->seq & 1];
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->stream, S.ev_back, 0));
+    HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray, S.c.mbits, h->g, h->p.ithresh, h->stream));
+    HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, h->stream));
+    HIP_OK(hipEventRecord(S.ev_ccl, h->stream));
+    HIP_OK(hipStreamWaitEvent(h->s_back, S.ev_ccl, 0));
     dvc::BackArgs a{};
     a.g = h->g;
     a.bgr = d;
     a.pitch = dp;
+    a.fstride = fstride;
     a.acc = h->acc;
     a.overlay = ov;
     a.compressed = cp;
     a.opitch = 3 * h->p.width;
-    a.kbits = S.kbits;
+    a.ostride = ostride;
+    a.kbits = S.c.kbits;
+    a.n = n;
     a.ksize = h->p.ksize;
     a.anchor = h->p.anchor;
     a.alpha = h->p.alpha;
     a.beta = h->p.beta;
     a.gamma = h->p.gamma;
     a.quant = h->p.quant;
+    {
+        const float z = std::rint(std::fmaf(0.0f, h->p.alpha, std::fmaf(0.0f, h->p.beta, h->p.gamma)));
+        a.acc0_fixed = z < 0.5f && z > -0.5f;  // saturate_cast<uchar>(0) == 0 (NaN/negatives excluded)
+    }
     a.M = h->M;
     a.stats = h->stats;
     a.dbg_dil = h->dbg_dil;
-    return a;
-}
-
-// Graph building: capture one stage on the private capture stream and add it as
-// a child-graph node that depends on `deps` (single-stream captures only).
-template <typename F>
-static int add_stage_node(dvc_fd* h, F&& enqueue, const hipGraphNode_t* deps, size_t ndeps, hipGraphNode_t* node)
-{
-    hipGraph_t child = nullptr;
-    HIP_OK(hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeRelaxed));
-    hipError_t e = enqueue(h->cap_stream);
-    hipError_t e2 = hipStreamEndCapture(h->cap_stream, &child);
-    if (e != hipSuccess) {
-        if (child) (void)hipGraphDestroy(child);
-        return fail(DVC_E_HIP, "stage capture: %s", hipGetErrorString(e));
-    }
-    HIP_OK(e2);
-    hipError_t e3 = hipGraphAddChildGraphNode(node, h->graph, deps, ndeps, child);
-    (void)hipGraphDestroy(child);
-    HIP_OK(e3);
-    return DVC_OK;
-}
-
-extern "C" {
-
-int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay, uint8_t* compressed,
-                uint8_t* acc_out)
-{
-    if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
-    if (!h->primed) return fail(DVC_E_STATE, "dvc_fd_step before dvc_fd_prime");
-    if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    HIP_OK(hipSetDevice(h->device));
-    const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
-    const bool pipe = h->depth > 1;
-    const size_t W = h->p.width, H = h->p.height, N = W * H;
-    const uint8_t* d;
-    int dp;
-    int rc = stage_in(h, bgr, pitch, &d, &dp);
-    if (rc) return rc;
-    Slot& S = h->slot[h->seq % h->depth];
-    dvc::BackArgs a = back_args(h, S, d, dp, devp ? overlay : (overlay ? h->d_ov : nullptr),
-                                devp ? compressed : (compressed ? h->d_cp : nullptr));
-
-    if (h->capturing) {
-        // frame t = graph nodes F_t, C_t, B_t with the edges of the pipeline:
-        //   F_t <- F_{t-1} (gray chain), C_{t-D} (mask slot reuse)
-        //   C_t <- F_t, B_{t-D} (kept-mask slot reuse)
-        //   B_t <- C_t, B_{t-1} (accumulated-mask chain)
-        if (acc_out) return fail(DVC_E_UNSUPPORTED, "acc_out is not captured into graphs");
-        hipGraphNode_t deps[2];
-        size_t nd = 0;
-        if (h->last_front) deps[nd++] = h->last_front;
-        if (S.node_ccl) deps[nd++] = S.node_ccl;
-        hipGraphNode_t nf, nc, nb;
-        rc = add_stage_node(h, [&](hipStream_t s) { return stage_front(h, S, d, dp, s); }, deps, nd, &nf);
-        if (rc) return rc;
-        nd = 0;
-        deps[nd++] = nf;
-        if (S.node_back) deps[nd++] = S.node_back;
-        rc = add_stage_node(h, [&](hipStream_t s) { return stage_ccl(h, S, s); }, deps, nd, &nc);
-        if (rc) return rc;
-        nd = 0;
-        deps[nd++] = nc;
-        if (h->last_back) deps[nd++] = h->last_back;
-        rc = add_stage_node(h, [&](hipStream_t s) { return dvc::launch_back(a, h->p.block, s); }, deps, nd, &nb);
-        if (rc) return rc;
-        h->last_front = nf;
-        h->last_back = nb;
-        S.node_ccl = nc;
-        S.node_back = nb;
-        h->cur ^= 1;
-        h->frames++;
-        h->seq++;
-        return DVC_OK;
-    }
-
-    if (pipe) {
-        if (h->graph_dirty) {  // order after the replayed graph on the origin stream
-            HIP_OK(hipEventRecord(h->ev_fork, h->stream));
-            hipStream_t s[2 + MAX_DEPTH];
-            int n = all_streams(h, s);
-            for (int i = 1; i < n; ++i) HIP_OK(hipStreamWaitEvent(s[i], h->ev_fork, 0));
-            h->graph_dirty = false;
-        }
-        h->eager_dirty = true;
-    }
-    // front(t): its mask slot must have been released by the contour filter of frame t - depth
-    if (pipe && S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
-    HIP_OK(stage_front(h, S, d, dp, h->s_front));
-    if (pipe) {
-        HIP_OK(hipEventRecord(S.ev_front, h->s_front));
-        // contour filter(t): after front(t), and after back(t - depth) released the kept mask
-        HIP_OK(hipStreamWaitEvent(S.s_ccl, S.ev_front, 0));
-        if (S.recorded) HIP_OK(hipStreamWaitEvent(S.s_ccl, S.ev_back, 0));
-    }
-    HIP_OK(stage_ccl(h, S, S.s_ccl));
-    if (pipe) {
-        HIP_OK(hipEventRecord(S.ev_ccl, S.s_ccl));
-        HIP_OK(hipStreamWaitEvent(h->s_back, S.ev_ccl, 0));
-    }
-    // back(t): after the contour filter of t; the back chain is ordered on s_back (acc)
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
     if (timed) {
         while (h->ev.size() < h->ev_used + 2) {
@@ -520,87 +349,78 @@ int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay, u
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_back));
         h->ev_used += 2;
     }
-    if (pipe) HIP_OK(hipEventRecord(S.ev_back, h->s_back));
+    HIP_OK(hipEventRecord(S.ev_back, h->s_back));
     S.recorded = true;
-    if (acc_out && devp) HIP_OK(hipMemcpyAsync(acc_out, h->acc, N, hipMemcpyDeviceToDevice, h->s_back));
-    h->cur ^= 1;
-    h->frames++;
     h->seq++;
-    if (!devp) {
-        if (overlay) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, 3 * N, hipMemcpyDeviceToHost, h->stream));
-        if (compressed) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, 3 * N, hipMemcpyDeviceToHost, h->stream));
-        if (acc_out) HIP_OK(hipMemcpyAsync(h->h_acc, h->acc, N, hipMemcpyDeviceToHost, h->stream));
-        HIP_OK(hipStreamSynchronize(h->stream));
-        if (overlay) std::memcpy(overlay, h->h_ov, 3 * N);
-        if (compressed) std::memcpy(compressed, h->h_cp, 3 * N);
-        if (acc_out) std::memcpy(acc_out, h->h_acc, N);
-    }
+    h->frames += (uint64_t)n;
+    h->last_n = n;
     return DVC_OK;
 }
 
-int dvc_fd_graph_begin(dvc_fd* h)
+// n frames in chunks of max_batch; host pointers are staged through the pinned
+// buffers (each chunk completes before the call returns).
+static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstride, int n, uint8_t* overlay,
+                      uint8_t* compressed, size_t ostride, uint8_t* acc_out)
 {
-    if (!h) return fail(DVC_E_INVALID, "NULL handle");
-    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) return fail(DVC_E_STATE, "graph capture needs DVC_FLAG_DEVICE_PTRS");
-    if (!h->primed) return fail(DVC_E_STATE, "graph capture before dvc_fd_prime");
-    if (h->capturing) return fail(DVC_E_STATE, "already capturing");
+    if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
+    if (!h->primed) return fail(DVC_E_STATE, "step before dvc_fd_prime");
+    if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
+    const size_t W = h->p.width, H = h->p.height, N = W * H, row = 3 * W;
+    if (pitch < row || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (n > 1 && (fstride < pitch * (H - 1) + row || fstride % 4))
+        return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
+    if (n > 1 && (overlay || compressed) && (ostride < 3 * N || ostride % 4))
+        return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
-    // earlier eager frames must be complete: the graph waits on nothing outside itself
-    HIP_OK(sync_all(h));
-    h->eager_dirty = false;
-    if (!h->cap_stream) HIP_OK(hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
-    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
-    if (h->graph) (void)hipGraphDestroy(h->graph);
-    h->gexec = nullptr;
-    h->graph = nullptr;
-    HIP_OK(hipGraphCreate(&h->graph, 0));
-    h->last_front = h->last_back = nullptr;
-    for (Slot& s : h->slot) {
-        s.node_ccl = s.node_back = nullptr;
-        s.recorded = false;
-    }
-    h->capturing = true;
-    h->cap_cur = h->cur;
-    h->cap_frames = h->frames;
-    h->cap_seq = h->seq;
-    return DVC_OK;
-}
-
-int dvc_fd_graph_end(dvc_fd* h)
-{
-    if (!h || !h->capturing) return fail(DVC_E_STATE, "not capturing");
-    HIP_OK(hipSetDevice(h->device));
-    h->capturing = false;
-    uint64_t n = h->frames - h->cap_frames;
-    // building the graph only recorded work: restore the host-side state
-    h->frames = h->cap_frames;
-    const bool ok = n > 0 && h->cur == h->cap_cur && n % (uint64_t)h->depth == 0;
-    h->cur = h->cap_cur;
-    h->seq = h->cap_seq;
-    if (!ok) {
-        (void)hipGraphDestroy(h->graph);
-        h->graph = nullptr;
-        return fail(DVC_E_INVALID, "graph of %llu frames: must be a nonzero multiple of 2 and of the pipeline "
-                    "depth %d", (unsigned long long)n, h->depth);
-    }
-    HIP_OK(hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
-    h->cap_frames = n;
-    return DVC_OK;
-}
-
-int dvc_fd_graph_launch(dvc_fd* h)
-{
-    if (!h || !h->gexec) return fail(DVC_E_STATE, "no captured graph");
-    HIP_OK(hipSetDevice(h->device));
-    if (h->eager_dirty) {  // eager steps on the internal streams must finish first
+    const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
+    for (int f0 = 0; f0 < n; f0 += h->max_batch) {
+        const int m = std::min(h->max_batch, n - f0);
+        const uint8_t* in = bgr + (size_t)f0 * fstride;
+        uint8_t* ov = overlay ? overlay + (size_t)f0 * ostride : nullptr;
+        uint8_t* cp = compressed ? compressed + (size_t)f0 * ostride : nullptr;
+        if (devp) {
+            int rc = enqueue_batch(h, in, (int)pitch, fstride, m, ov, cp, ostride);
+            if (rc) return rc;
+            continue;
+        }
+        for (int t = 0; t < m; ++t)
+            for (size_t y = 0; y < H; ++y)
+                std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->stream));
+        int rc = enqueue_batch(h, h->d_in, (int)row, 3 * N, m, ov ? h->d_ov : nullptr, cp ? h->d_cp : nullptr, 3 * N);
+        if (rc) return rc;
+        if (ov) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_back));
+        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_back));
         HIP_OK(sync_all(h));
-        h->eager_dirty = false;
+        for (int t = 0; t < m; ++t) {
+            if (ov) std::memcpy(ov + (size_t)t * ostride, h->h_ov + (size_t)t * 3 * N, 3 * N);
+            if (cp) std::memcpy(cp + (size_t)t * ostride, h->h_cp + (size_t)t * 3 * N, 3 * N);
+        }
     }
-    HIP_OK(hipGraphLaunch(h->gexec, h->stream));
-    h->graph_dirty = h->depth > 1;
-    for (Slot& s : h->slot) s.recorded = false;
-    h->frames += h->cap_frames;
+    if (acc_out) {
+        if (devp) {
+            HIP_OK(hipMemcpyAsync(acc_out, h->acc, N, hipMemcpyDeviceToDevice, h->s_back));
+        } else {
+            HIP_OK(hipMemcpyAsync(h->h_acc, h->acc, N, hipMemcpyDeviceToHost, h->s_back));
+            HIP_OK(hipStreamSynchronize(h->s_back));
+            std::memcpy(acc_out, h->h_acc, N);
+        }
+    }
     return DVC_OK;
+}
+
+extern "C" {
+
+int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay, uint8_t* compressed,
+                uint8_t* acc_out)
+{
+    return run_frames(h, bgr, pitch, 0, 1, overlay, compressed, 0, acc_out);
+}
+
+int dvc_fd_step_batch(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, int n, uint8_t* overlay,
+                      uint8_t* compressed, size_t out_stride)
+{
+    return run_frames(h, bgr, pitch, frame_stride, n, overlay, compressed, out_stride, nullptr);
 }
 
 int dvc_fd_sync(dvc_fd* h)
@@ -634,12 +454,13 @@ int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* dst)
     HIP_OK(sync_all(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
     if (plane == DVC_PLANE_GRAY || plane == DVC_PLANE_ACC) {
-        HIP_OK(hipMemcpy(dst, plane == DVC_PLANE_GRAY ? h->gray[h->cur] : h->acc, N, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(dst, plane == DVC_PLANE_GRAY ? h->gray : h->acc, N, hipMemcpyDeviceToHost));
         return DVC_OK;
     }
-    const Slot& S = h->slot[(h->seq + h->depth - 1) % h->depth];  // the last stepped frame
-    const uint64_t* src = plane == DVC_PLANE_MOTION ? S.mbits
-                        : plane == DVC_PLANE_FILTERED ? S.kbits
+    // the last frame of the last batch
+    const dvc::CclBufs c = h->slot[(h->seq - 1) & 1].c.frame((size_t)h->last_n - 1, h->g);
+    const uint64_t* src = plane == DVC_PLANE_MOTION ? c.mbits
+                        : plane == DVC_PLANE_FILTERED ? c.kbits
                         : plane == DVC_PLANE_DILATED ? h->dbg_dil : nullptr;
     if (plane != DVC_PLANE_MOTION && plane != DVC_PLANE_FILTERED && plane != DVC_PLANE_DILATED)
         return fail(DVC_E_INVALID, "unknown plane %d", plane);
@@ -717,7 +538,7 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
     if (e == hipSuccess) e = hipMemset(stats, 0, 8 * 4 * 64);
     if (e == hipSuccess) {
         dvc::CclBufs c{mbits, fbits, rs, re, nfg, fpar, gpar, gE, area2, kept, stats};
-        e = dvc::launch_ccl(c, g, min_area2, s);
+        e = dvc::launch_ccl(c, g, 1, min_area2, s);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     unsigned long long st[4] = {0, 0, 0, 0}, slots[64 * 4];

@@ -1,5 +1,12 @@
 // fd_kernels.h — launch interface between the C-ABI host code (fd_api.hip) and
 // the gfx950 kernels (fd_kernels.hip). Internal; not part of include/dvc.h.
+//
+// Every launch covers a BATCH of n consecutive frames of one feed. The only
+// true recurrences of the reference loop (fd:85-138) are prev_gray (fd:133) and
+// accumulated_mask (fd:107); both are elementwise, so k_front and k_back walk
+// the batch's frames in order inside each tile with that state in registers,
+// while the contour filter of every frame of the batch (independent given the
+// motion masks) runs as one grid with the frame in blockIdx.y.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,9 +29,10 @@ struct DctMat {
     float m[64];  // BxB row-major orthonormal DCT-II basis M[k][n], float32
 };
 
-// Device buffers of the contour-filter stage of one feed.
+// Device buffers of the contour-filter stage: frame f of a batch owns the f-th
+// slice of each array (sizes per frame below, see frame()).
 struct CclBufs {
-    const uint64_t* mbits;  // H x WW motion mask
+    uint64_t* mbits;        // H x WW motion mask
     uint64_t* fbits;        // H x WW filled mask (not-E)
     uint16_t *rs, *re;      // H x CAP run starts / ends
     uint32_t* nfg;          // H runs per row
@@ -33,31 +41,52 @@ struct CclBufs {
     uint8_t* gE;            // H x (CAP+1) gap is outside (1) / hole (0)
     uint32_t* area2;        // H x CAP 2*area per root
     uint64_t* kbits;        // H x WW kept (filtered) mask
-    unsigned long long* stats;  // 64 slots x 4 counters
+    unsigned long long* stats;  // 64 slots x 4 counters (shared by all frames)
+
+    __host__ __device__ static size_t bits_per_frame(const RowGeom& g) { return (size_t)g.H * g.WW; }
+    __host__ __device__ CclBufs frame(size_t f, const RowGeom& g) const
+    {
+        const size_t nb = (size_t)g.H * g.WW, nr = (size_t)g.H * g.CAP, ng = (size_t)g.H * (g.CAP + 1);
+        return CclBufs{mbits + f * nb, fbits + f * nb, rs + f * nr, re + f * nr, nfg + f * g.H, fpar + f * nr,
+                       gpar + f * (ng + 1), gE + f * ng, area2 + f * nr, kbits + f * nb, stats};
+    }
+    // bytes of every array for `frames` frames (host allocation)
+    static void sizes(const RowGeom& g, size_t frames, size_t out[10])
+    {
+        const size_t nb = (size_t)g.H * g.WW, nr = (size_t)g.H * g.CAP, ng = (size_t)g.H * (g.CAP + 1);
+        const size_t s[10] = {8 * nb, 8 * nb, 2 * nr, 2 * nr, 4 * (size_t)g.H, 4 * nr, 4 * (ng + 1), ng, 4 * nr, 8 * nb};
+        for (int i = 0; i < 10; ++i) out[i] = s[i] * frames;
+    }
 };
 
 struct BackArgs {
     RowGeom g;
-    const uint8_t* bgr;
+    const uint8_t* bgr;   // frame t at bgr + t * fstride, rows of `pitch` bytes
     int pitch;
-    uint8_t* acc;
-    uint8_t* overlay;     // nullable
-    uint8_t* compressed;  // nullable
+    size_t fstride;
+    uint8_t* acc;         // read before frame 0, written after frame n-1
+    uint8_t* overlay;     // nullable; frame t at overlay + t * ostride, rows of opitch
+    uint8_t* compressed;  // nullable; same layout
     int opitch;
-    const uint64_t* kbits;  // kept (filtered) mask from k_paint
+    size_t ostride;
+    const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
+    int n;                  // frames in the batch
     int ksize, anchor;
     float alpha, beta, gamma, quant;
+    int acc0_fixed;         // addWeighted(acc 0, dilated 0) == 0: zero blocks stay zero
     DctMat M;
     unsigned long long* stats;
-    uint64_t* dbg_dil;   // nullable: dilated mask bits
+    uint64_t* dbg_dil;   // nullable: dilated mask bits of frame n-1
 };
 
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
                         int W, int H, const GaussTaps& k, hipStream_t s);
-hipError_t launch_front(const uint8_t* bgr, int pitch, const uint8_t* prev, uint8_t* cur, uint64_t* mbits,
+// frames t = 0..n-1 at bgr + t*fstride; gray holds the previous blurred gray on
+// entry and frame n-1's on exit; motion mask of frame t -> mbits + t*H*WW
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, uint8_t* gray, uint64_t* mbits,
                         const RowGeom& g, int ithresh, hipStream_t s);
 int band_rows(const RowGeom& g);
-hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int64_t min_area2, hipStream_t s);
+hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
 hipError_t launch_back(const BackArgs& a, int block, hipStream_t s);
 
 }  // namespace dvc

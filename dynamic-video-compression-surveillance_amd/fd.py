@@ -58,14 +58,13 @@ def _addr(x) -> int:
 class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
                  device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
-                 pipeline: int = 1, **kwargs):
-        """``pipeline`` > 1 (device mode only) keeps that many frames in flight:
-        the contour filter of consecutive frames runs concurrently on internal
-        HIP streams while the front and back chains stay in frame order."""
+                 max_batch: int = 1, **kwargs):
+        """``max_batch``: frames one device launch covers in :meth:`step_batch`
+        (the contour-filter scratch is sized for 2 x max_batch frames)."""
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
             | (N.DVC_FLAG_KTIMING if ktiming else 0)
         self.params = derive_params(width, height, flags=flags, **kwargs)
-        self.params.pipeline = int(pipeline)
+        self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
@@ -112,17 +111,40 @@ class FDWorker:
                                       acc.ctypes.data if acc is not None else None))
         return overlay, compressed
 
-    # -------------------------------------------------------------- graphs --
-    def graph_begin(self) -> None:
-        """Start capturing device-mode steps into a hipGraph (see include/dvc.h)."""
-        N.check(self._lib.dvc_fd_graph_begin(self._h))
+    def step_batch(self, frames, overlay=None, compressed=None, want=("overlay", "compressed")):
+        """fd:85-138 for n consecutive frames (identical to n :meth:`step` calls).
 
-    def graph_end(self) -> None:
-        N.check(self._lib.dvc_fd_graph_end(self._h))
-
-    def graph_launch(self) -> None:
-        """Replay the captured frame sequence (asynchronous)."""
-        N.check(self._lib.dvc_fd_graph_launch(self._h))
+        Host mode: ``frames`` is an (n, H, W, 3) uint8 array; returns
+        ``(overlay, compressed)`` arrays of the same shape (allocated if not
+        given; a name missing from ``want`` is None). Device mode: ``frames``,
+        ``overlay``, ``compressed`` are (n, H, W, 3) uint8 device tensors or
+        ``(address, n)`` tuples of contiguous frames; asynchronous, returns None.
+        """
+        fs = 3 * self.W * self.H
+        if self.device_ptrs:
+            if isinstance(frames, tuple):
+                addr, n = int(frames[0]), int(frames[1])
+            else:
+                n = int(frames.shape[0])
+                addr = _addr(frames)
+            ov = _addr(overlay[0] if isinstance(overlay, tuple) else overlay) if overlay is not None else None
+            cp = _addr(compressed[0] if isinstance(compressed, tuple) else compressed) if compressed is not None else None
+            N.check(self._lib.dvc_fd_step_batch(self._h, addr, 3 * self.W, fs, n, ov, cp, fs))
+            return None
+        f = np.ascontiguousarray(frames)
+        if f.dtype != np.uint8 or f.ndim != 4 or f.shape[1:] != (self.H, self.W, 3):
+            raise ValueError(f"expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
+        if overlay is None and "overlay" in want:
+            overlay = np.empty_like(f)
+        if compressed is None and "compressed" in want:
+            compressed = np.empty_like(f)
+        for o in (overlay, compressed):
+            if o is not None and (o.shape != f.shape or o.dtype != np.uint8 or not o.flags.c_contiguous):
+                raise ValueError("output arrays must be contiguous uint8 of the frames' shape")
+        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, int(f.shape[0]),
+                                            overlay.ctypes.data if overlay is not None else None,
+                                            compressed.ctypes.data if compressed is not None else None, fs))
+        return overlay, compressed
 
     # ------------------------------------------------------------- queries --
     def sync(self) -> None:

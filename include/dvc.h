@@ -19,7 +19,7 @@
  *    the last error on the calling thread is available from dvc_last_error().
  *    The Python host turns a negative status into logging.error(...) and an
  *    early return, mirroring the reference's try/except (fd:140-145).
- *  - A handle is single-threaded (one feed, one HIP stream). Distinct handles may
+ *  - A handle is single-threaded (one feed). Distinct handles may
  *    be driven from distinct host threads concurrently.
  *  - Unless DVC_FLAG_DEVICE_PTRS is set, frame/output pointers are host memory
  *    and are staged through pinned buffers owned by the handle; with the flag they
@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 1
+#define DVC_ABI_VERSION 2
+#define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
 #define DVC_OK             0
@@ -71,7 +72,7 @@ extern "C" {
  *                 1-release_factor, 0 (fd:107).
  *   quant         quantization_level as float32 (fd:123).
  *   prime_ksize,prime_sigma  GaussianBlur of frame 0: 25, 30.0 (fd:77).
- *   pipeline      frames in flight (see the field).
+ *   max_batch     frames per device launch (see the field).
  */
 typedef struct dvc_fd_params {
     int32_t width;
@@ -88,10 +89,10 @@ typedef struct dvc_fd_params {
     int32_t prime_ksize;
     double prime_sigma;
     uint32_t flags;
-    uint32_t pipeline;  /* frames in flight: 0/1 = every launch in order on the
-                           handle's stream; 2..8 (DVC_FLAG_DEVICE_PTRS only) = the
-                           contour filter of consecutive frames overlapped on
-                           internal streams (front and back chains stay ordered) */
+    uint32_t max_batch; /* 0/1..DVC_MAX_BATCH: frames one device launch covers in
+                           dvc_fd_step_batch (longer calls are chunked). The
+                           contour-filter scratch (~18 MB per 1080p frame) is
+                           allocated for 2 x max_batch frames. */
 } dvc_fd_params;
 
 /* Cumulative per-handle counters (all frames stepped since create/prime). */
@@ -110,8 +111,10 @@ const char* dvc_last_error(void);
 int         dvc_device_count(int* count);
 
 /* Create a feed handle on `device`. `hip_stream` (a hipStream_t, may be NULL for
- * a stream owned by the handle) is the stream every launch of this handle is
- * enqueued on. Replaces the per-video setup at fd:56-82. */
+ * a stream owned by the handle) carries prime, the blur/threshold front and the
+ * contour filter; the back (dilate/accumulate/compress) runs on a second,
+ * internal stream so it overlaps the next batch's front. dvc_fd_sync waits for
+ * both. Replaces the per-video setup at fd:56-82. */
 int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
 
 /* Frame 0: gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77) -> previous
@@ -122,14 +125,27 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch);
  * threshold, findContours/contourArea/drawContours filter, dilate, addWeighted,
  * red overlay (fd:110-111) and the mask-gated block DCT quantisation with the
  * YCrCb round trip (fd:115-130). Outputs (each nullable, packed BGR of pitch
- * out_pitch = 3*W unless noted):
+ * 3*W unless noted):
  *   overlay     the frame written to dilated_motion_mask_video (fd:112)
  *   compressed  the frame written to compressed_final_video (fd:131)
  *   acc_out     the accumulated mask after this frame, H*W bytes (fd:107)
  * The call is asynchronous with respect to the host when DVC_FLAG_DEVICE_PTRS
- * is set; with host pointers it returns after the outputs have landed. */
+ * is set (dvc_fd_sync before reading outputs or reusing the input); with host
+ * pointers it returns after the outputs have landed. */
 int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch,
                 uint8_t* overlay, uint8_t* compressed, uint8_t* acc_out);
+
+/* n consecutive frames of the feed in one call (the reference loop fd:85-138
+ * run n times): frame t at bgr + t*frame_stride (rows of `pitch` bytes), its
+ * outputs at overlay/compressed + t*out_stride (rows of 3*W bytes; each
+ * nullable). Results are identical to n dvc_fd_step calls. Device launches
+ * cover max_batch frames each: the blur/threshold front and the dilate /
+ * accumulate / compress back walk the frames in order per tile (prev_gray and
+ * the accumulated mask stay on chip), the contour filter of every frame of the
+ * batch runs as one grid, and batch i+1's front overlaps batch i's back.
+ * Same synchronisation rules as dvc_fd_step. */
+int dvc_fd_step_batch(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, int n,
+                      uint8_t* overlay, uint8_t* compressed, size_t out_stride);
 
 /* Wait for every launch of the handle. */
 int dvc_fd_sync(dvc_fd* h);
@@ -140,7 +156,7 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out);
 /* Debug/parity access to the internal planes of the LAST stepped frame, each
  * H*W bytes written to host memory: 0 gray (blurred, fd:93), 1 motion mask
  * {0,255} (fd:97), 2 filtered mask {0,255} (fd:101-104), 3 accumulated mask
- * (fd:107), 4 dilated mask {0,255} (fd:106). Planes 2 and 4 need
+ * (fd:107), 4 dilated mask {0,255} (fd:106). Plane 4 needs
  * DVC_FLAG_KEEP_PLANES. Synchronises the handle. */
 #define DVC_PLANE_GRAY     0
 #define DVC_PLANE_MOTION   1
@@ -150,16 +166,8 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out);
 int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* host_dst);
 
 /* With DVC_FLAG_KTIMING: total milliseconds and launch count of the dominant
- * kernel since the last reset (synchronises the handle). reset!=0 clears. */
+ * kernel (k_back, one launch per batch) since the last reset (synchronises the handle). reset!=0 clears. */
 int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
-
-/* hipGraph capture of a sequence of device-pointer steps (DVC_FLAG_DEVICE_PTRS
- * only): begin, N x dvc_fd_step, end; each launch replays those N frames (one
- * graph launch instead of 6N kernel launches). The gray double buffer must be
- * back in its starting state at the end of the sequence, i.e. N even. */
-int dvc_fd_graph_begin(dvc_fd* h);
-int dvc_fd_graph_end(dvc_fd* h);
-int dvc_fd_graph_launch(dvc_fd* h);
 
 void dvc_fd_destroy(dvc_fd* h);
 
@@ -171,6 +179,39 @@ void dvc_fd_destroy(dvc_fd* h);
  * Synchronous; for the parity tests. */
 int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_area2,
                        int device, uint8_t* filtered, uint64_t* components);
+
+/* ---- optical-flow (OF) path ------------------------------------------------- */
+
+/*
+ * The per-frame worker of motion_compression_opt.py with its two passes fused
+ * in memory: temporal_smoothing_flow (of:65-101) produces the rectangle mask of
+ * frame t, compress_with_motion (of:141-185) compresses frame t with it. The
+ * reference round-trips both through lossy mp4v files in between (of:99-100,
+ * 121-122); the fused worker hands the exact mask and frame over instead.
+ *   flow_threshold, alpha_fraction, window, morph_kernel  of:29-31 kwargs
+ *                 (0.5, 0.2, 30, 2 as process_single_video_of passes, of:215-218)
+ *   pyr_scale..poly_sigma  calcOpticalFlowFarneback arguments (of:72-81)
+ *   quant         QTY_aggressive (100, of:138), 8x8 blocks on Y, Cr, Cb
+ */
+typedef struct dvc_of_params {
+    int32_t width;
+    int32_t height;
+    float flow_threshold;
+    float quant;
+    double alpha_fraction;
+    int32_t window;
+    int32_t morph_kernel;
+    double pyr_scale;
+    int32_t levels;
+    int32_t winsize;
+    int32_t iterations;
+    int32_t poly_n;
+    double poly_sigma;
+    uint32_t flags;      /* DVC_FLAG_DEVICE_PTRS */
+    uint32_t reserved;
+} dvc_of_params;
+
+typedef struct dvc_of dvc_of;
 
 /* The Q8 fixed-point Gaussian taps OpenCV's bit-exact 8U GaussianBlur uses
  * (getGaussianKernelBitExact + error-diffusion rounding to 8 fraction bits).

@@ -45,7 +45,7 @@ class FdParams(ctypes.Structure):
         ("prime_ksize", ctypes.c_int32),
         ("prime_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
-        ("pipeline", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
     ]
 
 
@@ -316,3 +316,137 @@ class OracleFD:
         s = FdStats()
         lib().oc_fd_get_stats(self._h, ctypes.byref(s))
         return {k: int(getattr(s, k)) for k, _ in FdStats._fields_}
+
+
+# ------------------------------------------------------------- optical flow --
+class OfParams(ctypes.Structure):
+    """Mirror of ``dvc_of_params`` (include/dvc.h)."""
+
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("flow_threshold", ctypes.c_float),
+        ("quant", ctypes.c_float),
+        ("alpha_fraction", ctypes.c_double),
+        ("window", ctypes.c_int32),
+        ("morph_kernel", ctypes.c_int32),
+        ("pyr_scale", ctypes.c_double),
+        ("levels", ctypes.c_int32),
+        ("winsize", ctypes.c_int32),
+        ("iterations", ctypes.c_int32),
+        ("poly_n", ctypes.c_int32),
+        ("poly_sigma", ctypes.c_double),
+        ("flags", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+    ]
+
+
+def of_params(width, height, flow_threshold=0.5, alpha_fraction=0.2, window_size=30, morph_kernel=2,
+              quant=100.0) -> OfParams:
+    """motion_compression_opt.py:29-31 kwargs + the hard-coded Farneback arguments (of:72-81)."""
+    p = OfParams()
+    p.width, p.height = int(width), int(height)
+    p.flow_threshold, p.quant = float(flow_threshold), float(quant)
+    p.alpha_fraction, p.window, p.morph_kernel = float(alpha_fraction), int(window_size), int(morph_kernel)
+    p.pyr_scale, p.levels, p.winsize, p.iterations, p.poly_n, p.poly_sigma = 0.3, 2, 9, 2, 5, 1.1
+    return p
+
+
+def _of_lib():
+    L = lib()
+    if not getattr(L, "_of_ready", False):
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        fp = ctypes.POINTER(ctypes.c_float)
+        L.oc_of_create.argtypes = [ctypes.POINTER(OfParams)]
+        L.oc_of_create.restype = ctypes.c_void_p
+        L.oc_of_destroy.argtypes = [ctypes.c_void_p]
+        L.oc_of_prime.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t]
+        L.oc_of_step.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, u8p, u8p, fp]
+        L.oc_of_read_plane.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p]
+        L.oc_farneback.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, fp]
+        L.oc_morph_close_open.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_rect_mask.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_rect_mask.restype = ctypes.c_int64
+        L.oc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, u8p]
+        L.oc_vote_threshold.argtypes = [ctypes.c_double, ctypes.c_int]
+        L.oc_fb_levels.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int]
+        L._of_ready = True
+    return L
+
+
+def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.3, levels=2, winsize=9, iterations=2, poly_n=5,
+              poly_sigma=1.1) -> np.ndarray:
+    prev, nxt = np.ascontiguousarray(prev, np.uint8), np.ascontiguousarray(nxt, np.uint8)
+    H, W = prev.shape
+    flow = np.empty((H, W, 2), np.float32)
+    _of_lib().oc_farneback(_u8(prev), _u8(nxt), W, H, pyr_scale, levels, winsize, iterations, poly_n, poly_sigma,
+                           flow.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return flow
+
+
+def morph_close_open(m: np.ndarray) -> np.ndarray:
+    m = np.ascontiguousarray(m, np.uint8)
+    out = np.empty_like(m)
+    _of_lib().oc_morph_close_open(_u8(m), m.shape[1], m.shape[0], _u8(out))
+    return out
+
+
+def rect_mask(m: np.ndarray):
+    m = np.ascontiguousarray(m, np.uint8)
+    out = np.empty_like(m)
+    n = _of_lib().oc_rect_mask(_u8(m), m.shape[1], m.shape[0], _u8(out))
+    return out, int(n)
+
+
+def of_compress(bgr: np.ndarray, mask: np.ndarray, quant=100.0) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr)
+    mask = np.ascontiguousarray(mask, np.uint8)
+    out = np.empty_like(bgr)
+    H, W = mask.shape
+    _of_lib().oc_of_compress(_u8(bgr), 3 * W, _u8(mask), W, H, quant, _u8(out))
+    return out
+
+
+def vote_threshold(alpha: float, L: int) -> int:
+    return int(_of_lib().oc_vote_threshold(alpha, L))
+
+
+class OracleOF:
+    """The oracle's fused OF worker (of:60-101 + of:141-185), one frame per ``step``."""
+
+    def __init__(self, width, height, **kwargs):
+        self.W, self.H = int(width), int(height)
+        self.params = of_params(width, height, **kwargs)
+        self._h = _of_lib().oc_of_create(ctypes.byref(self.params))
+        if not self._h:
+            raise ValueError("oracle rejected parameters")
+
+    def close(self):
+        if self._h:
+            _of_lib().oc_of_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def prime(self, bgr):
+        bgr = np.ascontiguousarray(bgr)
+        _of_lib().oc_of_prime(self._h, _u8(bgr), 3 * self.W)
+
+    def step(self, bgr):
+        bgr = np.ascontiguousarray(bgr)
+        mask = np.empty((self.H, self.W), np.uint8)
+        cp = np.empty_like(bgr)
+        flow = np.empty((self.H, self.W, 2), np.float32)
+        rc = _of_lib().oc_of_step(self._h, _u8(bgr), 3 * self.W, _u8(mask), _u8(cp),
+                                  flow.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if rc != 0:
+            raise RuntimeError(f"oracle OF step failed: {rc}")
+        return mask, cp, flow
+
+    def plane(self, which: int) -> np.ndarray:
+        """0 raw |flow| mask, 1 voted, 2 close/open, 3 rectangles."""
+        out = np.empty((self.H, self.W), np.uint8)
+        _of_lib().oc_of_read_plane(self._h, which, _u8(out))
+        return out

@@ -76,6 +76,28 @@ int oc_gauss_kernel_q8(int n, double sigma, uint16_t* taps)
 {
     if (n < 1 || n > 63 || (n & 1) == 0) return -1;
     double k[64];
+    oc_gauss_kernel_f64(n, sigma, k);
+    /* error-diffused rounding to Q8, mirrored, centre = 256 - sum(sides) */
+    int n2 = n / 2;
+    double err = 0.0;
+    int64_t sum = 0;
+    for (int i = 0; i < n2; ++i) {
+        double adj = k[i] * 256.0 + err;
+        double v0 = nearbyint(adj); /* cvRound(softdouble): round half to even */
+        err = adj - v0;
+        taps[i] = (uint16_t)v0;
+        taps[n - 1 - i] = (uint16_t)v0;
+        sum += (int64_t)v0;
+    }
+    sum *= 2;
+    taps[n2] = (uint16_t)(256 - sum);
+    return 0;
+}
+
+/* getGaussianKernelBitExact in double (the float kernels of getGaussianKernel
+ * are these values cast to float). n odd <= 63. */
+void oc_gauss_kernel_f64(int n, double sigma, double* k)
+{
     if (sigma <= 0 && n <= 7) {
         static const double t1[] = {1.0};
         static const double t3[] = {0.25, 0.5, 0.25};
@@ -105,21 +127,6 @@ int oc_gauss_kernel_q8(int n, double sigma, uint16_t* taps)
         }
         k[n2] = 1.0 * mul1;
     }
-    /* error-diffused rounding to Q8, mirrored, centre = 256 - sum(sides) */
-    int n2 = n / 2;
-    double err = 0.0;
-    int64_t sum = 0;
-    for (int i = 0; i < n2; ++i) {
-        double adj = k[i] * 256.0 + err;
-        double v0 = nearbyint(adj); /* cvRound(softdouble): round half to even */
-        err = adj - v0;
-        taps[i] = (uint16_t)v0;
-        taps[n - 1 - i] = (uint16_t)v0;
-        sum += (int64_t)v0;
-    }
-    sum *= 2;
-    taps[n2] = (uint16_t)(256 - sum);
-    return 0;
 }
 
 /*

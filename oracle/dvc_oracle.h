@@ -8,6 +8,7 @@
 int oc_reflect101(int x, int n);
 void oc_bgr2gray(const uint8_t* bgr, size_t pitch, int W, int H, uint8_t* gray);
 int oc_gauss_kernel_q8(int n, double sigma, uint16_t* taps);
+void oc_gauss_kernel_f64(int n, double sigma, double* k);
 void oc_gaussian_q8(const uint8_t* src, int W, int H, const uint16_t* k, int n, uint8_t* dst);
 void oc_absdiff_threshold(const uint8_t* a, const uint8_t* b, size_t n, int ithresh, uint8_t* m);
 int64_t oc_contour_filter(const uint8_t* mask, int W, int H, int64_t min_area2, uint8_t* filtered, uint8_t* filled);
@@ -32,4 +33,27 @@ int oc_fd_prime(oc_fd* h, const uint8_t* bgr, size_t pitch);
 int oc_fd_step(oc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay, uint8_t* compressed, uint8_t* acc_out);
 int oc_fd_read_plane(oc_fd* h, int plane, uint8_t* dst);
 void oc_fd_get_stats(oc_fd* h, dvc_fd_stats* out);
+
+/* optical-flow path (of_oracle.c) */
+void oc_blur_f32(const float* src, int W, int H, const float* k, int n, float* dst);
+void oc_resize_linear_f32(const float* src, int sw, int sh, int cn, float* dst, int dw, int dh);
+void oc_poly_gauss(int n, double sigma, float* g, float* xg, float* xxg, double* ig);
+void oc_poly_exp(const float* src, int W, int H, int n, double sigma, float* dst);
+void oc_update_matrices(const float* R0, const float* R1, const float* flow, int W, int H, float* M, int y0, int y1);
+void oc_update_flow_box(const float* M, int W, int H, int bs, float* flow);
+int oc_fb_levels(int W, int H, double pyr_scale, int levels);
+void oc_fb_level_poly(const uint8_t* gray, int W, int H, double pyr_scale, int k, int poly_n, double poly_sigma,
+                      float* R, int* lw, int* lh);
+void oc_farneback(const uint8_t* prev, const uint8_t* next, int W, int H, double pyr_scale, int levels,
+                  int winsize, int iterations, int poly_n, double poly_sigma, float* flow_out);
+void oc_morph_close_open(const uint8_t* src, int W, int H, uint8_t* dst);
+int64_t oc_rect_mask(const uint8_t* m, int W, int H, uint8_t* out);
+void oc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int W, int H, float q, uint8_t* out);
+int oc_vote_threshold(double alpha, int L);
+typedef struct oc_of oc_of;
+oc_of* oc_of_create(const dvc_of_params* p);
+void oc_of_destroy(oc_of* h);
+int oc_of_prime(oc_of* h, const uint8_t* bgr, size_t pitch);
+int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_t* compressed, float* flow);
+int oc_of_read_plane(oc_of* h, int which, uint8_t* dst);
 #endif

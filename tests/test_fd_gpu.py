@@ -139,65 +139,70 @@ def test_device_mode_matches_host_mode(gpu_lib):
     host.close()
 
 
-def test_graph_replay_matches_eager(gpu_lib):
-    """hipGraph capture of an even frame sequence == the same steps launched eagerly."""
+def _oracle_sequence(oracle, frames, **kw):
+    H, W = frames.shape[1:3]
+    ref = oracle.OracleFD(W, H, **kw)
+    ref.prime(frames[0])
+    ovs, cps = [], []
+    for t in range(1, len(frames)):
+        ov, cp, _ = ref.step(frames[t])
+        ovs.append(ov)
+        cps.append(cp)
+    planes = {name: ref.plane(idx) for name, idx in PLANES.items()}
+    st = ref.stats()
+    ref.close()
+    return np.stack(ovs), np.stack(cps), planes, st
+
+
+@pytest.mark.parametrize("W,H,n,max_batch,noisy", [
+    (640, 360, 13, 5, True),      # chunks 5, 5, 2
+    (640, 360, 9, 8, False),
+    (1920, 1080, 6, 4, True),     # chunks 4, 1
+])
+def test_batch_matches_oracle(gpu_lib, oracle_lib, W, H, n, max_batch, noisy):
+    """dvc_fd_step_batch (host mode): every frame's outputs, the last frame's planes
+    and the stats equal the oracle's frame-by-frame run."""
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, n, seed=3, noisy=noisy)
+    rov, rcp, rplanes, rst = _oracle_sequence(oracle_lib, frames)
+    w = gpu_lib.FDWorker(W, H, keep_planes=True, max_batch=max_batch)
+    w.prime(frames[0])
+    ov, cp = w.step_batch(frames[1:])
+    for t in range(n - 1):
+        assert np.array_equal(ov[t], rov[t]), f"overlay differs at frame {t + 1}"
+        assert np.array_equal(cp[t], rcp[t]), f"compressed differs at frame {t + 1}"
+    for name, idx in PLANES.items():
+        assert np.array_equal(w.plane(idx), rplanes[name]), f"{name} plane differs"
+    assert w.stats() == rst
+    w.close()
+
+
+def test_batch_device_matches_steps(gpu_lib):
+    """Device-mode batches (several calls, overlapping slots) == one step per frame."""
     import torch
     from dvc_amd.synthetic import clip
-    frames = torch.from_numpy(clip(640, 360, 5, seed=4)).to("cuda:0")
-    order = [1, 2, 3, 4, 3, 2]          # ping-pong after frame 0
+    frames = clip(640, 360, 8, seed=6, noisy=True)
+    order = [1, 2, 3, 4, 5, 6, 7, 6, 5, 4, 3, 2, 1, 2, 3, 4, 5]
+    seq = torch.from_numpy(np.ascontiguousarray(frames[order])).to("cuda:0")
+    f0 = torch.from_numpy(frames[0]).to("cuda:0")
     outs = []
-    for use_graph in (False, True):
-        ov = torch.empty((len(order), 360, 640, 3), dtype=torch.uint8, device="cuda:0")
-        cp = torch.empty_like(ov)
-        w = gpu_lib.FDWorker(640, 360, device_ptrs=True)
-        w.prime(frames[0])
-        if use_graph:
-            w.graph_begin()
-        for j, t in enumerate(order):
-            w.step(frames[t], ov[j], cp[j])
-        if use_graph:
-            w.graph_end()
-            w.graph_launch()
-            w.graph_launch()      # second pass: state carries over exactly as eager would
+    for mode in ("step", "batch"):
+        ov = torch.empty_like(seq)
+        cp = torch.empty_like(seq)
+        w = gpu_lib.FDWorker(640, 360, device_ptrs=True, max_batch=3)
+        w.prime(f0)
+        if mode == "step":
+            for j in range(len(order)):
+                w.step(seq[j], ov[j], cp[j])
         else:
-            for j, t in enumerate(order):
-                w.step(frames[t], ov[j], cp[j])
+            for a, b in ((0, 7), (7, 8), (8, 17)):      # chunks 3,3,1 | 1 | 3,3,3
+                w.step_batch(seq[a:b], ov[a:b], cp[a:b])
         w.sync()
-        outs.append((ov.cpu().numpy(), cp.cpu().numpy(), w.stats()))
+        outs.append((ov.cpu().numpy(), cp.cpu().numpy(), w.stats(), w.plane(PLANES["acc"])))
         w.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2]
-
-
-@pytest.mark.parametrize("depth", [2, 3])
-def test_pipelined_matches_sequential(gpu_lib, depth):
-    """Frames in flight on internal streams (eager and hipGraph) == in-order launches."""
-    import torch
-    from dvc_amd.synthetic import clip
-    frames = torch.from_numpy(clip(640, 360, 8, seed=6, noisy=True)).to("cuda:0")
-    order = [1, 2, 3, 4, 5, 6, 7, 6, 5, 4, 3, 2]       # 12 steps: multiple of 2 and of depth
-    outs = []
-    for mode in ("seq", "pipe", "pipe_graph"):
-        ov = torch.empty((len(order), 360, 640, 3), dtype=torch.uint8, device="cuda:0")
-        cp = torch.empty_like(ov)
-        w = gpu_lib.FDWorker(640, 360, device_ptrs=True, pipeline=1 if mode == "seq" else depth)
-        w.prime(frames[0])
-        for rep in range(2):
-            if mode == "pipe_graph" and rep == 0:
-                w.graph_begin()
-            if mode == "pipe_graph" and rep == 1:
-                w.graph_end()
-                w.graph_launch()
-                w.graph_launch()
-                break
-            for j, t in enumerate(order):
-                w.step(frames[t], ov[j], cp[j])
-        w.sync()
-        outs.append((ov.cpu().numpy(), cp.cpu().numpy(), w.stats()))
-        w.close()
-    for o in outs[1:]:
-        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
-        assert outs[0][2] == o[2]
+    assert np.array_equal(outs[0][3], outs[1][3])
 
 
 def test_errors(gpu_lib):
