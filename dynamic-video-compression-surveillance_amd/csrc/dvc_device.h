@@ -85,18 +85,6 @@ __device__ __forceinline__ int wave_incl_scan(int v)
     return v;
 }
 
-// first index in [0,n) with a[i] >= v (n if none), a ascending
-template <typename T>
-__device__ __forceinline__ int lower_bound(const T* a, int n, int v)
-{
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if ((int)a[mid] < v) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 __device__ __forceinline__ int popc_range(const uint64_t* b, int s, int e)
 {
     if (s > e) return 0;
@@ -156,28 +144,94 @@ inline __device__ void lunion(uint32_t* lp, uint32_t a, uint32_t b)
     }
 }
 
-// Overlapping runs / gaps of rows y and y+1 -> union (callback gets local or global ids).
-template <typename FG, typename BG>
-__device__ __forceinline__ void row_pair_unions(const RowGeom& g, const uint16_t* rs0, const uint16_t* re0, int n0,
-                                                const uint16_t* rs1, const uint16_t* re1, int n1, FG fg, BG bg)
+// Run index of one mask row (in LDS): start / end bit words of its maximal
+// foreground runs and their exclusive prefix counts (pre[w] = set bits in
+// words < w, pre[WW] = runs in the row). Run k = [select(st, k), select(en, k)].
+struct RowIdx {
+    const uint64_t* st;
+    const uint64_t* en;
+    const uint16_t* ps;
+    const uint16_t* pe;
+};
+
+// number of set bits at positions <= x
+__device__ __forceinline__ int rank_le(const uint64_t* b, const uint16_t* pre, int WW, int x)
+{
+    if (x < 0) return 0;
+    const int w = x >> 6;
+    if (w >= WW) return pre[WW];
+    return pre[w] + __popcll(b[w] & (~0ull >> (63 - (x & 63))));
+}
+
+// position of the k-th (0-based) set bit, k < pre[WW]
+__device__ __forceinline__ int select_k(const uint64_t* b, const uint16_t* pre, int WW, int k)
+{
+    int lo = 0, hi = WW - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)pre[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    uint64_t v = b[lo];
+    for (int r = k - (int)pre[lo]; r > 0; --r) v &= v - 1;
+    return lo * 64 + __builtin_ctzll(v);
+}
+
+// One wave: run index of mask row `row` (global, WW words) into LDS; returns
+// the run count; *motion (nullable) = this lane's share of the row's set pixels.
+__device__ __forceinline__ int build_row_idx(const uint64_t* row, int WW, int W, uint64_t* st, uint64_t* en,
+                                             uint16_t* ps, uint16_t* pe, unsigned long long* motion)
 {
     const int lane = threadIdx.x & 63;
-    // foreground, 8-connectivity: [a,b] ~ [c,d] iff c <= b+1 && d >= a-1
-    for (int i = lane; i < n0; i += 64) {
-        const int a = rs0[i], b = re0[i];
-        for (int j = lower_bound(re1, n1, a - 1); j < n1 && (int)rs1[j] <= b + 1; ++j) fg(i, j);
-    }
-    // background, 4-connectivity between non-empty gaps
-    for (int i = lane; i <= n0; i += 64) {
-        const int ga = i == 0 ? 0 : (int)re0[i - 1] + 1;
-        const int gb = i == n0 ? g.W - 1 : (int)rs0[i] - 1;
-        if (ga > gb) continue;
-        for (int j = lower_bound(rs1, n1, ga + 1); j <= n1; ++j) {  // first gap whose end >= ga
-            const int ca = j == 0 ? 0 : (int)re1[j - 1] + 1;
-            if (ca > gb) break;
-            const int cb = j == n1 ? g.W - 1 : (int)rs1[j] - 1;
-            if (ca <= cb) bg(i, j);
+    int ns = 0, ne = 0;
+    unsigned long long m = 0;
+    for (int b0 = 0; b0 < WW; b0 += 64) {
+        const int i = b0 + lane;
+        const int ic = min(i, WW - 1);
+        const uint64_t w0 = row[ic], pw0 = row[max(ic - 1, 0)], nw0 = row[min(ic + 1, WW - 1)];
+        const uint64_t w = i < WW ? w0 : 0, pw = i > 0 && i < WW ? pw0 : 0, nw = i + 1 < WW ? nw0 : 0;
+        const uint64_t s = w & ~((w << 1) | (pw >> 63));
+        const uint64_t e = w & ~((w >> 1) | (nw << 63));
+        const int cs = __popcll(s), ce = __popcll(e);
+        const int is = wave_incl_scan(cs), ie = wave_incl_scan(ce);
+        if (i < WW) {
+            st[i] = s;
+            en[i] = e;
+            ps[i] = (uint16_t)(ns + is - cs);
+            pe[i] = (uint16_t)(ne + ie - ce);
         }
+        ns += __shfl(is, 63, 64);
+        ne += __shfl(ie, 63, 64);
+        m += (unsigned long long)__popcll(w);
+    }
+    if (lane == 0) {
+        ps[WW] = (uint16_t)ns;
+        pe[WW] = (uint16_t)ne;
+    }
+    if (motion) *motion = m;
+    return ns;
+}
+
+// Unions between the runs (8-connected) and the gaps (4-connected) of two
+// consecutive rows r0 (above) and r1, by rank queries on their run indexes:
+//   run i = [a,b] touches runs j of r1 with re1[j] >= a-1 and rs1[j] <= b+1;
+//   gap i = [a,b] overlaps gaps j of r1 with rs1[j] >= a+1 (or j = n1) and
+//   re1[j-1] <= b-1 (or j = 0).
+template <typename FG, typename BG>
+__device__ __forceinline__ void row_pair_unions(int W, int WW, const RowIdx& r0, int n0, const RowIdx& r1, FG fg,
+                                                BG bg)
+{
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < n0; i += 64) {
+        const int a = select_k(r0.st, r0.ps, WW, i), b = select_k(r0.en, r0.pe, WW, i);
+        const int j0 = rank_le(r1.en, r1.pe, WW, a - 2), j1 = rank_le(r1.st, r1.ps, WW, b + 1);
+        for (int j = j0; j < j1; ++j) fg(i, j);
+    }
+    for (int i = lane; i <= n0; i += 64) {
+        const int a = i == 0 ? 0 : select_k(r0.en, r0.pe, WW, i - 1) + 1;
+        const int b = i == n0 ? W - 1 : select_k(r0.st, r0.ps, WW, i) - 1;
+        if (a > b) continue;
+        const int j0 = rank_le(r1.st, r1.ps, WW, a), j1 = rank_le(r1.en, r1.pe, WW, b - 1);
+        for (int j = j0; j <= j1; ++j) bg(i, j);
     }
 }
 

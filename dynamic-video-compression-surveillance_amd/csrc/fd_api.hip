@@ -96,6 +96,7 @@ void dct_matrix(int B, float* M)
 // Contour-filter scratch of one batch in flight (max_batch frames).
 struct Slot {
     dvc::CclBufs c{};
+    uint64_t *rbits = nullptr, *sbits = nullptr;   // k_acc -> k_out bits
     hipEvent_t ev_ccl = nullptr, ev_back = nullptr;
     bool recorded = false;  // ev_back holds a batch that the next user of the slot must wait for
 };
@@ -111,12 +112,15 @@ struct dvc_fd {
     dvc::DctMat M{};
     bool primed = false;
     int max_batch = 1;
+    int SW = 0;          // 64-block words per block row
+    size_t sstride = 0;  // static-block bit words per frame
     uint64_t frames = 0, seq = 0;  // frames stepped, batches launched
     int last_n = 0;                // frames of the last batch
     // Two slots: the front + contour filter of batch i+1 overlap the back of batch i.
     Slot slot[2];
     // device state
-    uint8_t* gray = nullptr;       // previous blurred gray (fd:77, 133)
+    uint8_t* gray[2] = {nullptr, nullptr};  // previous blurred gray (fd:77, 133): gray[gcur]
+    int gcur = 0;
     uint8_t* acc = nullptr;        // accumulated mask (fd:81, 107)
     uint64_t* dbg_dil = nullptr;
     uint32_t* tmp32 = nullptr;
@@ -133,13 +137,14 @@ struct dvc_fd {
 static void free_all(dvc_fd* h)
 {
     for (Slot& s : h->slot) {
-        void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE};
+        void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE,
+                       s.rbits, s.sbits};
         for (void* p : dev)
             if (p) (void)hipFree(p);
         for (hipEvent_t e : {s.ev_ccl, s.ev_back})
             if (e) (void)hipEventDestroy(e);
     }
-    void* dev[] = {h->gray, h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
+    void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     void* pin[] = {h->h_in, h->h_ov, h->h_cp, h->h_acc};
@@ -206,6 +211,8 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->g.H = p.height;
     h->g.WW = (p.width + 63) / 64;
     h->g.CAP = p.width / 2 + 1;
+    h->SW = (p.width / p.block + 63) / 64;
+    h->sstride = (size_t)(p.height / p.block) * h->SW;
     if (gauss_taps(p.prime_ksize, p.prime_sigma, h->kprime.t) != 0) {
         delete h;
         return fail(DVC_E_INVALID, "prime blur size %d must be odd, 1..63", p.prime_ksize);
@@ -237,11 +244,13 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
                            (void**)&s.c.area2, (void**)&s.c.kbits};
         for (int i = 0; i < 10; ++i)
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = dalloc(&s.rbits, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         for (hipEvent_t* ev : {&s.ev_ccl, &s.ev_back})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
     struct { void** ptr; size_t bytes; } allocs[] = {
-        {(void**)&h->gray, N}, {(void**)&h->acc, N}, {(void**)&h->stats, 8 * 4 * 64},
+        {(void**)&h->gray[0], N}, {(void**)&h->gray[1], N}, {(void**)&h->acc, N}, {(void**)&h->stats, 8 * 4 * 64},
     };
     for (auto& a : allocs)
         if ((e = dalloc(a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
@@ -284,7 +293,7 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
         d = h->d_in;
         dp = (int)(3 * W);
     }
-    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray, h->p.width, h->p.height, h->kprime, h->stream));
+    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->gcur], h->p.width, h->p.height, h->kprime, h->stream));
     HIP_OK(hipMemsetAsync(h->acc, 0, N, h->stream));
     HIP_OK(hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
@@ -306,7 +315,9 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
 {
     Slot& S = h->slot[h->seq & 1];
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->stream, S.ev_back, 0));
-    HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray, S.c.mbits, h->g, h->p.ithresh, h->stream));
+    HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], S.c.mbits, h->g,
+                             h->p.ithresh, h->stream));
+    h->gcur ^= 1;
     HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, h->stream));
     HIP_OK(hipEventRecord(S.ev_ccl, h->stream));
     HIP_OK(hipStreamWaitEvent(h->s_back, S.ev_ccl, 0));
@@ -321,6 +332,10 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.opitch = 3 * h->p.width;
     a.ostride = ostride;
     a.kbits = S.c.kbits;
+    a.rbits = S.rbits;
+    a.sbits = S.sbits;
+    a.SW = h->SW;
+    a.sstride = h->sstride;
     a.n = n;
     a.ksize = h->p.ksize;
     a.anchor = h->p.anchor;
@@ -335,6 +350,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.M = h->M;
     a.stats = h->stats;
     a.dbg_dil = h->dbg_dil;
+    // KTIMING: events around k_out (the HBM-bound kernel): k_acc | ev | k_out | ev
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
     if (timed) {
         while (h->ev.size() < h->ev_used + 2) {
@@ -342,9 +358,8 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
             HIP_OK(hipEventCreate(&e));
             h->ev.push_back(e);
         }
-        HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_back));
     }
-    HIP_OK(dvc::launch_back(a, h->p.block, h->s_back));
+    HIP_OK(dvc::launch_back(a, h->p.block, h->s_back, timed ? h->ev[h->ev_used] : nullptr));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_back));
         h->ev_used += 2;
@@ -454,7 +469,7 @@ int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* dst)
     HIP_OK(sync_all(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
     if (plane == DVC_PLANE_GRAY || plane == DVC_PLANE_ACC) {
-        HIP_OK(hipMemcpy(dst, plane == DVC_PLANE_GRAY ? h->gray : h->acc, N, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(dst, plane == DVC_PLANE_GRAY ? h->gray[h->gcur] : h->acc, N, hipMemcpyDeviceToHost));
         return DVC_OK;
     }
     // the last frame of the last batch

@@ -70,6 +70,10 @@ struct BackArgs {
     int opitch;
     size_t ostride;
     const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
+    uint64_t* rbits;        // acc > 127 per pixel, H x WW per frame (k_acc -> k_out)
+    uint64_t* sbits;        // acc all zero per block, (H/B) x SW per frame (k_acc -> k_out)
+    int SW;                 // 64-block words per block row = ceil(W/B/64)
+    size_t sstride;         // (H/B) * SW
     int n;                  // frames in the batch
     int ksize, anchor;
     float alpha, beta, gamma, quant;
@@ -81,12 +85,13 @@ struct BackArgs {
 
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
                         int W, int H, const GaussTaps& k, hipStream_t s);
-// frames t = 0..n-1 at bgr + t*fstride; gray holds the previous blurred gray on
-// entry and frame n-1's on exit; motion mask of frame t -> mbits + t*H*WW
-hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, uint8_t* gray, uint64_t* mbits,
-                        const RowGeom& g, int ithresh, hipStream_t s);
+// frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
+// gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+                        uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
 int band_rows(const RowGeom& g);
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
-hipError_t launch_back(const BackArgs& a, int block, hipStream_t s);
+// k_acc then k_out; `mid` (nullable) is recorded between them
+hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t mid);
 
 }  // namespace dvc

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dvc_device.h"
 #include "fd_kernels.h"
 
@@ -68,13 +70,18 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 // ------------------------------------------------------------------ front ---
 // Tile: 256 px (64 lanes x 4 px) x 16 rows; 4 waves. Gray halo 2 px / 2 rows,
 // loaded as 66 quads x 20 rows with BORDER_REFLECT_101 at the image edges.
-// The workgroup walks the batch's frames in order: the previous blurred gray of
-// its 4x4 px per lane stays in registers (fd:133), and frame t+1's BGR loads
-// are issued as soon as frame t's gray is in LDS, so they fly under t's blur.
+// The workgroup walks a chunk of the batch's frames in order: the previous
+// blurred gray of its 4x4 px per lane stays in registers (fd:133), and frame
+// t+1's BGR loads are issued as soon as frame t's gray is in LDS, so they fly
+// under t's blur. blockIdx.z = chunk of `chunk` frames: chunk 0 starts from the
+// previous batch's gray (gray_in), chunk c > 0 first re-derives frame
+// c*chunk-1's blurred gray (a warm-up pass that emits no mask) — more
+// workgroups in flight for one extra frame read per chunk.
 constexpr int FT_W = 256, FT_H = 16, FT_Q = FT_W / 4 + 2, FT_R = FT_H + 4;
 
 __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
-                                               uint8_t* __restrict__ gray, uint64_t* __restrict__ mbits,
+                                               int chunk, const uint8_t* __restrict__ gray_in,
+                                               uint8_t* __restrict__ gray_out, uint64_t* __restrict__ mbits,
                                                int W, int H, int WW, int ithresh)
 {
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
@@ -83,6 +90,8 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const int x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H;
     const int x = x0 + 4 * lane;
     const size_t mstride = (size_t)H * WW;
+    const int t_first = blockIdx.z * chunk, t_end = min(n, t_first + chunk);
+    const int t_begin = blockIdx.z == 0 ? 0 : t_first - 1;   // warm-up frame for c > 0
 
     // Every load below is unconditional from a clamped, always-valid address
     // (the value is discarded where it is not needed): a conditional load makes
@@ -93,7 +102,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
 #pragma unroll
     for (int i = 0; i < FT_H / 4; ++i) {
         const int y = min(y0 + wave + 4 * i, H - 1);
-        pv[i] = *reinterpret_cast<const uint32_t*>(gray + (size_t)y * W + xc);
+        pv[i] = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * W + xc);
     }
     // BGR of the 20 halo rows: wave w loads rows w, w+4, ..; lane l its quad l
     // (12 contiguous bytes), lanes 0/1 also the left/right halo quads.
@@ -112,7 +121,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
             h0[j] = q[0]; h1[j] = q[1]; h2[j] = q[2];
         }
     };
-    load(bgr);
+    load(bgr + (size_t)t_begin * fstride);
 
     // BORDER_REFLECT_101 columns: the halo quad left of x = 0 and the quad at
     // x = W (when it lies in this tile) are byte permutations of their
@@ -120,7 +129,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const bool fix_l = x0 == 0;
     const int qe = (W - x0) / 4 + 1;              // LDS quad index of px W
     const bool fix_r = qe < FT_Q;
-    for (int t = 0; t < n; ++t) {
+    for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int r = wave + 4 * j;
@@ -144,7 +153,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
         }
         __syncthreads();
         // next frame (the last frame reloads itself: an unconditional load)
-        load(bgr + (size_t)min(t + 1, n - 1) * fstride);
+        load(bgr + (size_t)min(t + 1, t_end - 1) * fstride);
 
 #pragma unroll
         for (int i = 0; i < (FT_R * 64 + 255) / 256; ++i) {
@@ -181,31 +190,34 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
                 nib |= (uint32_t)(d > ithresh) << j;
             }
             pv[i] = g;
-            if (y >= H || x >= W) nib = 0;
+            if (y >= H || x >= W || t < t_first) nib = 0;
             unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
             w |= __shfl_xor(w, 1, 64);
             w |= __shfl_xor(w, 2, 64);
             w |= __shfl_xor(w, 4, 64);
             w |= __shfl_xor(w, 8, 64);
             const int wi = (x0 >> 6) + (lane >> 4);
-            if ((lane & 15) == 0 && y < H && wi < WW) mb[(size_t)y * WW + wi] = w;
+            if ((lane & 15) == 0 && y < H && wi < WW && t >= t_first) mb[(size_t)y * WW + wi] = w;
         }
     }
     // frame n-1's blurred gray becomes the previous gray of the next batch
+    if (t_end == n) {
 #pragma unroll
-    for (int i = 0; i < FT_H / 4; ++i) {
-        const int y = y0 + wave + 4 * i;
-        if (y < H && x < W) *reinterpret_cast<uint32_t*>(gray + (size_t)y * W + x) = pv[i];
+        for (int i = 0; i < FT_H / 4; ++i) {
+            const int y = y0 + wave + 4 * i;
+            if (y < H && x < W) *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * W + x) = pv[i];
+        }
     }
 }
 
 // ------------------------------------------------------------------- band ---
-// One workgroup per band of BH rows (one wave per row): extract the row's
-// foreground runs straight from the bit mask, then union-find in LDS over the
-// band's runs (8-connected) and gaps (4-connected; gaps on the image border
-// joined to the OUTSIDE node), flatten, and publish every run/gap's band-local
-// root as a global id. Local ids: 0 = OUTSIDE, fg (r,k) = 1 + r*CAP + k,
-// gap (r,k) = 1 + BH*CAP + r*(CAP+1) + k. Dynamic LDS: local parents.
+// One workgroup per band of BH rows (one wave per row): build the row's run
+// index (start/end bit words + prefix counts, in LDS) straight from the bit
+// mask and write its runs to global, then union-find in LDS over the band's
+// runs (8-connected) and gaps (4-connected; gaps on the image border joined to
+// the OUTSIDE node), flatten, and publish every run/gap's band-local root as a
+// global id. Local ids: 0 = OUTSIDE, fg (r,k) = 1 + r*CAP + k,
+// gap (r,k) = 1 + BH*CAP + r*(CAP+1) + k. Dynamic LDS: see band_lds().
 __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -217,42 +229,38 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
     uint32_t* __restrict__ gpar = fb.gpar;
     uint32_t* __restrict__ area2 = fb.area2;
     unsigned long long* __restrict__ stats = fb.stats;
-    extern __shared__ __attribute__((aligned(16))) uint32_t lp[];
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int WW = g.WW, W = g.W;
+    uint64_t* l_st = lds;
+    uint64_t* l_en = l_st + BH * WW;
+    uint32_t* lp = reinterpret_cast<uint32_t*>(l_en + BH * WW);
+    uint16_t* l_ps = reinterpret_cast<uint16_t*>(lp + BH * (2 * g.CAP + 1) + 1);
+    uint16_t* l_pe = l_ps + BH * (WW + 1);
     __shared__ int s_n[32];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int y0 = blockIdx.x * BH, y = y0 + wave;
     const bool act = y < g.H;
     const uint32_t CAP = (uint32_t)g.CAP, FG0 = 1, GP0 = 1 + (uint32_t)BH * CAP;
     const uint32_t base = (uint32_t)y * CAP;
+    uint64_t* st = l_st + wave * WW;
+    uint64_t* en = l_en + wave * WW;
+    uint16_t* ps = l_ps + wave * (WW + 1);
+    uint16_t* pe = l_pe + wave * (WW + 1);
 
-    // ---- phase 1: runs of row y (bit tricks + wave scan), written to global
+    // ---- phase 1: run index of row y in LDS; runs to global (later kernels)
     int n = 0;
-    bool left_bg = true, right_bg = true;
     unsigned long long motion = 0;
     if (act) {
-        const uint64_t* row = mbits + (size_t)y * g.WW;
-        int ne = 0;
-        for (int b0 = 0; b0 < g.WW; b0 += 64) {
-            const int i = b0 + lane;
-            uint64_t w = 0, pw = 0, nw = 0;
-            if (i < g.WW) {
-                w = row[i];
-                pw = i > 0 ? row[i - 1] : 0;
-                nw = i + 1 < g.WW ? row[i + 1] : 0;
-            }
-            uint64_t st = w & ~((w << 1) | (pw >> 63));
-            uint64_t en = w & ~((w >> 1) | (nw << 63));
-            const int cs = __popcll(st), ce = __popcll(en);
-            const int ps = wave_incl_scan(cs), pe = wave_incl_scan(ce);
-            int ks = n + ps - cs, ke = ne + pe - ce;
-            while (st) { rs[base + ks++] = (uint16_t)(i * 64 + __ffsll((unsigned long long)st) - 1); st &= st - 1; }
-            while (en) { re[base + ke++] = (uint16_t)(i * 64 + __ffsll((unsigned long long)en) - 1); en &= en - 1; }
-            n += __shfl(ps, 63, 64);
-            ne += __shfl(pe, 63, 64);
-            motion += (unsigned long long)__popcll(w);
+        const uint64_t* row = mbits + (size_t)y * WW;
+        n = build_row_idx(row, WW, W, st, en, ps, pe, &motion);
+        for (int i = lane; i < WW; i += 64) {
+            uint64_t s = st[i], e = en[i];
+            int ks = ps[i], ke = pe[i];
+            while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
+            while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
         }
-        left_bg = !(row[0] & 1ull);
-        right_bg = !((row[(g.W - 1) >> 6] >> ((g.W - 1) & 63)) & 1ull);
+        const bool left_bg = !(st[0] & 1ull);
+        const bool right_bg = !((en[(W - 1) >> 6] >> ((W - 1) & 63)) & 1ull);
         for (int k = lane; k < n; k += 64) lp[FG0 + wave * CAP + k] = FG0 + wave * CAP + k;
         for (int k = lane; k <= n; k += 64) {
             const bool nonempty = (k == 0) ? left_bg : (k == n ? right_bg : true);
@@ -267,12 +275,12 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
     if (lane == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
     __syncthreads();
 
-    // ---- phase 2: unions between the band's consecutive rows, in LDS
+    // ---- phase 2: unions between the band's consecutive rows, all in LDS
     if (act && wave + 1 < BH && y + 1 < g.H) {
-        const int n1 = s_n[wave + 1];
         const uint32_t f0 = FG0 + wave * CAP, f1 = f0 + CAP;
         const uint32_t q0 = GP0 + wave * (CAP + 1), q1 = q0 + CAP + 1;
-        row_pair_unions(g, rs + base, re + base, n, rs + base + CAP, re + base + CAP, n1,
+        const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
+        row_pair_unions(W, WW, r0, n, r1,
                         [&](int i, int j) { lunion(lp, f0 + i, f1 + j); },
                         [&](int i, int j) { lunion(lp, q0 + i, q1 + j); });
     }
@@ -302,21 +310,28 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
 }
 
 // ------------------------------------------------------------------ merge ---
-// One wave per band seam (rows b*BH-1 and b*BH): global unions of the band
-// roots, with monotone atomicMin links (uf_union).
+// One wave per band seam (rows b*BH-1 and b*BH): run indexes of both rows in
+// LDS, then global unions of the band roots with monotone atomicMin links.
 __global__ void __launch_bounds__(64) k_merge(CclBufs cb, RowGeom g, int BH)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
-    const uint16_t* __restrict__ rs = fb.rs;
-    const uint16_t* __restrict__ re = fb.re;
-    const uint32_t* __restrict__ nfg = fb.nfg;
     uint32_t* fpar = fb.fpar;
     uint32_t* gpar = fb.gpar;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int WW = g.WW;
     const int y = (blockIdx.x + 1) * BH - 1;
     if (y + 1 >= g.H) return;
+    uint64_t* st = lds;
+    uint64_t* en = st + 2 * WW;
+    uint16_t* ps = reinterpret_cast<uint16_t*>(en + 2 * WW);
+    uint16_t* pe = ps + 2 * (WW + 1);
+    const int n0 = build_row_idx(fb.mbits + (size_t)y * WW, WW, g.W, st, en, ps, pe, nullptr);
+    build_row_idx(fb.mbits + (size_t)(y + 1) * WW, WW, g.W, st + WW, en + WW, ps + WW + 1, pe + WW + 1, nullptr);
+    __syncthreads();
     const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
     const uint32_t g0 = 1u + (uint32_t)y * (g.CAP + 1), g1 = g0 + (g.CAP + 1);
-    row_pair_unions(g, rs + b0, re + b0, (int)nfg[y], rs + b1, re + b1, (int)nfg[y + 1],
+    const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
+    row_pair_unions(g.W, WW, r0, n0, r1,
                     [&](int i, int j) { uf_union(fpar, b0 + i, b1 + j); },
                     [&](int i, int j) { uf_union(gpar, g0 + i, g1 + j); });
 }
@@ -418,110 +433,118 @@ __global__ void __launch_bounds__(64) k_area(CclBufs cb, RowGeom g)
     const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
     const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
     int comps = 0;
-    for (int k = lane; k < n; k += 64) {
-        uint32_t id = base + k;
-        uint32_t r = uf_find(fpar, id);
-        atomicMin(fpar + id, r);
-        comps += r == id;
-        if (last) continue;
-        int s = rs[id], e = re[id];
-        int c = 2 * popc_range(b, s, e);
-        if (k == 0 || ge[k]) {
-            int bs = bit_at(b, s);
-            c -= bs;
-            if (s >= 1 && bs && bit_at(b, s - 1)) c += 1;
+    for (int k0 = 0; k0 < n; k0 += 64) {   // uniform trip count: the wave reduces below
+        const int k = k0 + lane;
+        const bool valid = k < n;
+        const uint32_t id = base + (valid ? k : 0);
+        uint32_t r = 0xffffffffu;
+        int c = 0;
+        if (valid) {
+            r = uf_find(fpar, id);
+            atomicMin(fpar + id, r);
+            comps += r == id;
         }
-        if (k == n - 1 || ge[k + 1]) {
-            int be = bit_at(b, e);
-            c -= be;
-            if (e <= g.W - 2 && be && bit_at(b, e + 1)) c += 1;
+        if (valid && !last) {
+            int s = rs[id], e = re[id];
+            c = 2 * popc_range(b, s, e);
+            if (k == 0 || ge[k]) {
+                int bs = bit_at(b, s);
+                c -= bs;
+                if (s >= 1 && bs && bit_at(b, s - 1)) c += 1;
+            }
+            if (k == n - 1 || ge[k + 1]) {
+                int be = bit_at(b, e);
+                c -= be;
+                if (e <= g.W - 2 && be && bit_at(b, e + 1)) c += 1;
+            }
+            if (k + 1 < n && !ge[k + 1]) c += 2 * popc_range(b, e + 1, (int)rs[id + 1] - 1);
         }
-        if (k + 1 < n && !ge[k + 1]) c += 2 * popc_range(b, e + 1, (int)rs[id + 1] - 1);
-        if (c) atomicAdd(area2 + r, (uint32_t)c);
+        // one atomic per run of lanes with the same root (a large component's
+        // runs of a row would otherwise all hit one address)
+        const uint32_t rp = __shfl_up(r, 1, 64);
+        const bool head = lane == 0 || rp != r;
+        const unsigned long long heads = __ballot(head);
+        const unsigned long long after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+        const int seg_end = after ? __builtin_ctzll(after) - 1 : 63;
+        const int incl = wave_incl_scan(c);
+        const int seg = __shfl(incl, seg_end, 64) - incl + c;
+        if (head && valid && seg) atomicAdd(area2 + r, (uint32_t)seg);
     }
     for (int d = 32; d >= 1; d >>= 1) comps += __shfl_xor(comps, d, 64);
     if (lane == 0 && comps) atomicAdd(stats + STAT_SLOT(y) * 4 + 2, (unsigned long long)comps);
 }
 
 // ------------------------------------------------------------------- back ---
-// Tile: 64 blocks across (64*B px) x 4 block rows (4*B rows), one wave per
-// block row, one lane per BxB block. Kept-mask window rows [y0-anchor,
-// y0+4B-1+ksize-1-anchor], words [x0/64-1, x0/64+B] in LDS.
-// The workgroup walks the batch's frames in order with its blocks of the
-// accumulated mask in registers (fd:107 is an elementwise recurrence): acc is
-// read once before frame 0 and written once after frame n-1. Frame t+1's kept
-// mask and BGR loads are issued right after frame t's kept mask is in LDS.
-template <int B>
-__global__ void __launch_bounds__(256) k_back(BackArgs a)
+// The back of the loop is split at its only recurrence:
+//   k_acc  (sequential over the batch's frames, per tile) 7x7 dilate of the
+//          kept mask (fd:106) and the accumulated-mask update (fd:107) with
+//          acc in registers; per frame it emits only bits: acc > 127 per pixel
+//          (rbits, the overlay's red mask, fd:110) and "acc all zero" per
+//          block (sbits, fd:117)
+//   k_out  (one grid over tiles x frames, no recurrence) red overlay
+//          (fd:110-111) and the static-block DCT quantisation with the YCrCb
+//          round trip (fd:115-130) from the BGR frame and those bits
+//
+// k_acc tile: one wave = 64 blocks across (64*B px) x 1 block row (B rows);
+// kept-mask window rows [y0-anchor, y0+B-1+ksize-1-anchor], words
+// [x0/64-1, x0/64+B] in LDS. The windows are loaded 8 frames per burst, the
+// next burst in flight while the current one is processed.
+template <int B, int KIT, int KMAX>
+__global__ void __launch_bounds__(64) k_acc(BackArgs a)
 {
-    constexpr int TW = 64 * B, TH = 4 * B, NWD = B + 2, MAXR = TH + 63;
-    __shared__ unsigned long long s_k[MAXR][NWD];   // kept (filtered) mask window
+    constexpr int NWD = B + 2, MAXR = B + KMAX - 1;   // KMAX >= ksize
+    __shared__ unsigned long long s_k[MAXR][NWD];   // kept mask window
     __shared__ unsigned long long s_h[MAXR][B];     // horizontally dilated
-    __shared__ unsigned long long s_v[TH][B];       // dilated
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
-    const int k = a.ksize, an = a.anchor, NR = TH + k - 1;
+    __shared__ unsigned long long s_v[B][B];        // dilated
+    const int lane = threadIdx.x;
+    const int x0 = blockIdx.x * 64 * B, y0 = blockIdx.y * B;
+    const int k = a.ksize, an = a.anchor, NR = B + k - 1;
     const int wx0 = (x0 >> 6) - 1;
     const int W = a.g.W, H = a.g.H, WW = a.g.WW;
     const size_t kstride = (size_t)H * WW;
 
-    // All loads are unconditional from clamped, always-valid addresses, then
-    // selected (a conditional load drains vmcnt to 0, see k_front).
-    constexpr int KIT = (MAXR * NWD + 255) / 256;
     size_t koff[KIT];
     bool kok[KIT];
 #pragma unroll
     for (int i = 0; i < KIT; ++i) {
-        const int idx = tid + 256 * i, r = idx / NWD, c = idx - r * NWD, gy = y0 - an + r, gw = wx0 + c;
+        const int idx = lane + 64 * i, r = idx / NWD, c = idx - r * NWD, gy = y0 - an + r, gw = wx0 + c;
         kok[i] = idx < NR * NWD && gy >= 0 && gy < H && gw >= 0 && gw < WW;
         koff[i] = (size_t)clampi(gy, 0, H - 1) * WW + clampi(gw, 0, WW - 1);
     }
-    const int bx = x0 + lane * B, by = y0 + wave * B;
-    const bool active = bx < W && by < H;
-    const int bxc = min(bx, W - B), byc = min(by, H - B);
-    uint32_t acv[B][B / 4];   // this lane's block of the accumulated mask
+    const int bx = x0 + lane * B;
+    const bool active = bx < W;
+    const int bxc = min(bx, W - B);
+    uint32_t acv[B][B / 4];
 #pragma unroll
     for (int i = 0; i < B; ++i) {
-        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(byc + i) * W + bxc);
+        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(y0 + i) * W + bxc);
 #pragma unroll
         for (int d = 0; d < B / 4; ++d) acv[i][d] = ac[d];
     }
-    unsigned long long kw[KIT];
-    uint32_t px[B][3 * B / 4], pxn[B][3 * B / 4];   // BGR, B px per row = 3B/4 dwords
-    auto load_k = [&](int t) {
-        const uint64_t* kb = a.kbits + (size_t)t * kstride;
+    // kept-mask windows of U frames per load burst, two bursts in flight
+    constexpr int U = KIT >= 8 ? 1 : 8 / KIT;
+    unsigned long long kA[U][KIT], kB[U][KIT];
+    auto load_chunk = [&](int t0, unsigned long long (&dst)[U][KIT]) {
 #pragma unroll
-        for (int i = 0; i < KIT; ++i) kw[i] = kb[koff[i]];
-    };
-    auto load_px = [&](int t, uint32_t (&dst)[B][3 * B / 4]) {
-        const uint8_t* f = a.bgr + (size_t)t * a.fstride;
+        for (int u = 0; u < U; ++u) {
+            const uint64_t* kb = a.kbits + (size_t)min(t0 + u, a.n - 1) * kstride;   // clamped: unconditional
 #pragma unroll
-        for (int i = 0; i < B; ++i) {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(byc + i) * a.pitch + 3 * bxc);
-#pragma unroll
-            for (int d = 0; d < 3 * B / 4; ++d) dst[i][d] = src[d];
+            for (int i = 0; i < KIT; ++i) dst[u][i] = kb[koff[i]];
         }
     };
-    load_k(0);
-    load_px(0, px);
     unsigned long long nstatic = 0;
 
-    for (int t = 0; t < a.n; ++t) {
+    auto frame = [&](int t, const unsigned long long (&kw)[KIT]) {
 #pragma unroll
         for (int i = 0; i < KIT; ++i) {
-            const int idx = tid + 256 * i;
+            const int idx = lane + 64 * i;
             if (idx < NR * NWD) s_k[idx / NWD][idx % NWD] = kok[i] ? kw[i] : 0ull;
         }
         __syncthreads();
-        // next frame's loads (the last frame reloads itself: unconditional)
-        const int tn = min(t + 1, a.n - 1);
-        load_k(tn);
-        load_px(tn, pxn);
-
         // horizontal dilation: out bit x = OR src bits x-an .. x+k-1-an
-        for (int i = tid; i < NR * B; i += 256) {
-            int r = i / B, c = i % B + 1;
-            uint64_t pv = s_k[r][c - 1], cv = s_k[r][c], nv = s_k[r][c + 1];
+        for (int i = lane; i < NR * B; i += 64) {
+            const int r = i / B, c = i % B + 1;
+            const uint64_t pv = s_k[r][c - 1], cv = s_k[r][c], nv = s_k[r][c + 1];
             uint64_t o = 0;
             for (int off = -an; off <= k - 1 - an; ++off) {
                 if (off == 0) o |= cv;
@@ -531,166 +554,210 @@ __global__ void __launch_bounds__(256) k_back(BackArgs a)
             s_h[r][c - 1] = o;
         }
         __syncthreads();
-        for (int i = tid; i < TH * B; i += 256) {
-            int rr = i / B, c = i % B;
+        if (lane < B * B) {
+            const int rr = lane / B, c = lane % B;
             uint64_t o = 0;
             for (int j = 0; j < k; ++j) o |= s_h[rr + j][c];
             s_v[rr][c] = o;
         }
         __syncthreads();
-        if (a.dbg_dil && t == a.n - 1) {
-            for (int i = tid; i < TH * B; i += 256) {
-                int rr = i / B, c = i % B, gy = y0 + rr, gw = (x0 >> 6) + c;
-                if (gy < H && gw < WW) a.dbg_dil[(size_t)gy * WW + gw] = s_v[rr][c];
-            }
+        if (a.dbg_dil && t == a.n - 1 && lane < B * B) {
+            const int rr = lane / B, c = lane % B, gw = (x0 >> 6) + c;
+            if (gw < WW) a.dbg_dil[(size_t)(y0 + rr) * WW + gw] = s_v[rr][c];
         }
-
-        // per-block work: wave -> block row, lane -> block
-        uint32_t dwv[B], dor = 0, aor = 0;   // dilated bits of the block's rows; any set / any acc
+        uint32_t dwv[B], dor = 0, aor = 0;
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            dwv[i] = (uint32_t)(s_v[wave * B + i][(lane * B) >> 6] >> ((lane * B) & 63)) & ((1u << B) - 1);
+            dwv[i] = (uint32_t)(s_v[i][(lane * B) >> 6] >> ((lane * B) & 63)) & ((1u << B) - 1);
             dor |= dwv[i];
 #pragma unroll
             for (int d = 0; d < B / 4; ++d) aor |= acv[i][d];
         }
-        // accumulated mask (fd:107); an all-zero block with no dilated pixel stays
-        // all zero when addWeighted(0, 0) = 0 (a.acc0_fixed), skipping the float math
-        bool is_static = true;
+        // addWeighted (fd:107); an all-zero block with no dilated pixel stays all
+        // zero when addWeighted(0, 0) = 0 (a.acc0_fixed), skipping the float math
+        bool zero = true;
         if (!(a.acc0_fixed && dor == 0 && aor == 0)) {
 #pragma unroll
-            for (int i = 0; i < B; ++i) {
+            for (int i = 0; i < B; ++i)
 #pragma unroll
                 for (int d = 0; d < B / 4; ++d) {
                     uint32_t av = acv[i][d], nv = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        float dil = (float)(((dwv[i] >> (4 * d + j)) & 1u) ? 255 : 0);
-                        float tv = __builtin_fmaf((float)((av >> (8 * j)) & 255), a.alpha,
-                                                  __builtin_fmaf(dil, a.beta, a.gamma));
-                        float rr = __builtin_rintf(tv);
-                        uint32_t v = rr < 0.f ? 0u : (rr > 255.f ? 255u : (uint32_t)rr);
+                        const float dil = (float)(((dwv[i] >> (4 * d + j)) & 1u) ? 255 : 0);
+                        const float tv = __builtin_fmaf((float)((av >> (8 * j)) & 255), a.alpha,
+                                                        __builtin_fmaf(dil, a.beta, a.gamma));
+                        const float rr = __builtin_rintf(tv);
+                        const uint32_t v = rr < 0.f ? 0u : (rr > 255.f ? 255u : (uint32_t)rr);
                         nv |= v << (8 * j);
                     }
                     acv[i][d] = nv;
-                    is_static = is_static && nv == 0;
+                    zero = zero && nv == 0;
                 }
-            }
         }
-        if (active) {
-            // overlay (fd:110-111): (0,0,255) where acc > 127
-            if (a.overlay) {
-                uint8_t* ovf = a.overlay + (size_t)t * a.ostride;
-                uint32_t red = 0;
+        // bits out: acc > 127 per pixel, all-zero per block
+        uint64_t* rb = a.rbits + (size_t)t * kstride;
+        constexpr int LPW = 64 / B;   // lanes per 64-px word
 #pragma unroll
-                for (int i = 0; i < B; ++i)
+        for (int i = 0; i < B; ++i) {
+            uint32_t m = 0;
 #pragma unroll
-                    for (int d = 0; d < B / 4; ++d) red |= acv[i][d] & 0x80808080u;
-#pragma unroll
-                for (int i = 0; i < B; ++i) {
-                    uint32_t ow[3 * B / 4];
-                    if (!red) {
-#pragma unroll
-                        for (int d = 0; d < 3 * B / 4; ++d) ow[d] = px[i][d];
-                    } else {
-                        uint8_t ob[3 * B];
-#pragma unroll
-                        for (int j = 0; j < B; ++j) {
-                            uint32_t av = (acv[i][j >> 2] >> (8 * (j & 3))) & 255;
-#pragma unroll
-                            for (int c = 0; c < 3; ++c) {
-                                int bi = 3 * j + c;
-                                uint32_t v = (px[i][bi >> 2] >> (8 * (bi & 3))) & 255;
-                                ob[bi] = av > 127 ? (c == 2 ? 255 : 0) : (uint8_t)v;
-                            }
-                        }
-#pragma unroll
-                        for (int d = 0; d < 3 * B / 4; ++d)
-                            ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-                    }
-                    uint32_t* o = reinterpret_cast<uint32_t*>(ovf + (size_t)(by + i) * a.opitch + 3 * bx);
-#pragma unroll
-                    for (int d = 0; d < 3 * B / 4; ++d) o[d] = ow[d];
-                }
+            for (int d = 0; d < B / 4; ++d) {
+                const uint32_t hb = acv[i][d] & 0x80808080u;   // bit 7 of each byte
+                m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * d);
             }
-            // compressed (fd:115-130): BGR -> YCrCb; static block: Y' = trunc(clip(IDCT(
-            // rint(DCT(Y - 128) / q) q) + 128)), Cr = Cb = 128 -> (Y', Y', Y'); otherwise
-            // the YCrCb -> BGR round trip of the pixels
-            if (a.compressed) {
-                uint8_t* cpf = a.compressed + (size_t)t * a.ostride;
-                uint32_t cw[B][3 * B / 4];
-                if (is_static) {
-                    float X[B * B];
+            unsigned long long w = (unsigned long long)(active ? m : 0u) << (B * (lane % LPW));
 #pragma unroll
-                    for (int i = 0; i < B; ++i)
-#pragma unroll
-                        for (int j = 0; j < B; ++j) {
-                            int b = (px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
-                            int gg = (px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
-                            int r = (px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
-                            // 1868 + 9617 + 4899 = 2^14: Y of u8 input is in 0..255, no saturation
-                            X[i * B + j] = (float)descale14(b * 1868 + gg * 9617 + r * 4899) - 128.0f;
-                        }
-                    block_dct_quant<B>(X, a.M, a.quant);
-#pragma unroll
-                    for (int i = 0; i < B; ++i) {
-                        uint8_t ob[3 * B];
-#pragma unroll
-                        for (int j = 0; j < B; ++j) {
-                            float v = X[i * B + j] + 128.0f;
-                            v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
-                            ob[3 * j] = ob[3 * j + 1] = ob[3 * j + 2] = (uint8_t)(uint32_t)v;
-                        }
-#pragma unroll
-                        for (int d = 0; d < 3 * B / 4; ++d)
-                            cw[i][d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < B; ++i) {
-                        uint8_t ob[3 * B];
-#pragma unroll
-                        for (int j = 0; j < B; ++j) {
-                            int b = (px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
-                            int gg = (px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
-                            int r = (px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
-                            int yv = descale14(b * 1868 + gg * 9617 + r * 4899);
-                            int cr = (int)satu8(descale14((r - yv) * 11682 + (128 << 14))) - 128;
-                            int cb = (int)satu8(descale14((b - yv) * 9241 + (128 << 14))) - 128;
-                            ob[3 * j] = (uint8_t)satu8(yv + descale14(cb * 29049));
-                            ob[3 * j + 1] = (uint8_t)satu8(yv + descale14(cb * -5636 + cr * -11698));
-                            ob[3 * j + 2] = (uint8_t)satu8(yv + descale14(cr * 22987));
-                        }
-#pragma unroll
-                        for (int d = 0; d < 3 * B / 4; ++d)
-                            cw[i][d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < B; ++i) {
-                    uint32_t* o = reinterpret_cast<uint32_t*>(cpf + (size_t)(by + i) * a.opitch + 3 * bx);
-#pragma unroll
-                    for (int d = 0; d < 3 * B / 4; ++d) o[d] = cw[i][d];
-                }
-            }
+            for (int sft = 1; sft < LPW; sft <<= 1) w |= __shfl_xor(w, sft, 64);
+            const int wi = (x0 >> 6) + lane / LPW;
+            if (lane % LPW == 0 && wi < WW) rb[(size_t)(y0 + i) * WW + wi] = w;
         }
-        nstatic += (unsigned long long)__popcll(__ballot(active && is_static));
+        const unsigned long long sb = __ballot(active && zero);
+        if (lane == 0) a.sbits[(size_t)t * a.sstride + (size_t)blockIdx.y * a.SW + blockIdx.x] = sb;
+        nstatic += (unsigned long long)__popcll(sb);
+    };
+
+    load_chunk(0, kA);
+    for (int t0 = 0; t0 < a.n; t0 += 2 * U) {
+        load_chunk(t0 + U, kB);
 #pragma unroll
-        for (int i = 0; i < B; ++i)
+        for (int u = 0; u < U; ++u)
+            if (t0 + u < a.n) frame(t0 + u, kA[u]);
+        load_chunk(t0 + 2 * U, kA);
 #pragma unroll
-            for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = pxn[i][d];
+        for (int u = 0; u < U; ++u)
+            if (t0 + U + u < a.n) frame(t0 + U + u, kB[u]);
     }
+
     // the accumulated mask after frame n-1 (fd:107)
     if (active) {
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(by + i) * W + bx);
+            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(y0 + i) * W + bx);
 #pragma unroll
             for (int d = 0; d < B / 4; ++d) ac[d] = acv[i][d];
         }
     }
-    if (lane == 0 && nstatic)
-        atomicAdd(a.stats + STAT_SLOT(blockIdx.x * 4 + blockIdx.y * 7 + wave) * 4 + 3, nstatic);
+    if (lane == 0 && nstatic) atomicAdd(a.stats + STAT_SLOT(blockIdx.x * 7 + blockIdx.y) * 4 + 3, nstatic);
+}
+
+// k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
+// row, one lane per BxB block; blockIdx.z = frame of the batch.
+template <int B>
+__global__ void __launch_bounds__(256) k_out(BackArgs a)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = blockIdx.z;
+    const int W = a.g.W, H = a.g.H, WW = a.g.WW;
+    const int bx = blockIdx.x * 64 * B + lane * B, by = (blockIdx.y * 4 + wave) * B;
+    if (bx >= W || by >= H) return;   // no barrier below
+    const uint8_t* f = a.bgr + (size_t)t * a.fstride;
+    uint32_t px[B][3 * B / 4];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * a.pitch + 3 * bx);
+#pragma unroll
+        for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
+    }
+    const bool is_static =
+        (a.sbits[(size_t)t * a.sstride + (size_t)(by / B) * a.SW + (bx / B >> 6)] >> ((bx / B) & 63)) & 1ull;
+    // overlay (fd:110-111): (0,0,255) where acc > 127
+    if (a.overlay) {
+        uint32_t red[B], rany = 0;
+        const uint64_t* rb = a.rbits + (size_t)t * H * WW;
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            red[i] = (uint32_t)(rb[(size_t)(by + i) * WW + (bx >> 6)] >> (bx & 63)) & ((1u << B) - 1);
+            rany |= red[i];
+        }
+        uint8_t* ovf = a.overlay + (size_t)t * a.ostride;
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            uint32_t ow[3 * B / 4];
+            if (!rany) {
+#pragma unroll
+                for (int d = 0; d < 3 * B / 4; ++d) ow[d] = px[i][d];
+            } else {
+                uint8_t ob[3 * B];
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    const bool r = (red[i] >> j) & 1u;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const int bi = 3 * j + c;
+                        const uint32_t v = (px[i][bi >> 2] >> (8 * (bi & 3))) & 255;
+                        ob[bi] = r ? (c == 2 ? 255 : 0) : (uint8_t)v;
+                    }
+                }
+#pragma unroll
+                for (int d = 0; d < 3 * B / 4; ++d)
+                    ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
+            }
+            uint32_t* o = reinterpret_cast<uint32_t*>(ovf + (size_t)(by + i) * a.opitch + 3 * bx);
+#pragma unroll
+            for (int d = 0; d < 3 * B / 4; ++d) o[d] = ow[d];
+        }
+    }
+    // compressed (fd:115-130): BGR -> YCrCb; static block: Y' = trunc(clip(IDCT(
+    // rint(DCT(Y - 128) / q) q) + 128)), Cr = Cb = 128 -> (Y', Y', Y'); otherwise
+    // the YCrCb -> BGR round trip of the pixels
+    if (a.compressed) {
+        uint8_t* cpf = a.compressed + (size_t)t * a.ostride;
+        uint32_t cw[B][3 * B / 4];
+        if (is_static) {
+            float X[B * B];
+#pragma unroll
+            for (int i = 0; i < B; ++i)
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    const int b = (px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
+                    const int gg = (px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
+                    const int r = (px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+                    // 1868 + 9617 + 4899 = 2^14: Y of u8 input is in 0..255, no saturation
+                    X[i * B + j] = (float)descale14(b * 1868 + gg * 9617 + r * 4899) - 128.0f;
+                }
+            block_dct_quant<B>(X, a.M, a.quant);
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                uint8_t ob[3 * B];
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    float v = X[i * B + j] + 128.0f;
+                    v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+                    ob[3 * j] = ob[3 * j + 1] = ob[3 * j + 2] = (uint8_t)(uint32_t)v;
+                }
+#pragma unroll
+                for (int d = 0; d < 3 * B / 4; ++d)
+                    cw[i][d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                uint8_t ob[3 * B];
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    const int b = (px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
+                    const int gg = (px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
+                    const int r = (px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+                    const int yv = descale14(b * 1868 + gg * 9617 + r * 4899);
+                    const int cr = (int)satu8(descale14((r - yv) * 11682 + (128 << 14))) - 128;
+                    const int cb = (int)satu8(descale14((b - yv) * 9241 + (128 << 14))) - 128;
+                    ob[3 * j] = (uint8_t)satu8(yv + descale14(cb * 29049));
+                    ob[3 * j + 1] = (uint8_t)satu8(yv + descale14(cb * -5636 + cr * -11698));
+                    ob[3 * j + 2] = (uint8_t)satu8(yv + descale14(cr * 22987));
+                }
+#pragma unroll
+                for (int d = 0; d < 3 * B / 4; ++d)
+                    cw[i][d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(cpf + (size_t)(by + i) * a.opitch + 3 * bx);
+#pragma unroll
+            for (int d = 0; d < 3 * B / 4; ++d) o[d] = cw[i][d];
+        }
+    }
 }
 
 // --------------------------------------------------------------- launchers --
@@ -704,42 +771,81 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, uint8_t* gray, uint64_t* mbits,
-                        const RowGeom& g, int ithresh, hipStream_t s)
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+                        uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
-    dim3 grid((g.W + FT_W - 1) / FT_W, (g.H + FT_H - 1) / FT_H);
-    hipLaunchKernelGGL(k_front, grid, dim3(256), 0, s, bgr, pitch, fstride, n, gray, mbits, g.W, g.H, g.WW, ithresh);
+    const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
+    // chunks: ~2560 workgroups in flight, at least 8 frames per chunk
+    int chunks = (2560 + tx * ty / 2) / (tx * ty);
+    chunks = std::max(1, std::min(chunks, n / 8));
+    const int chunk = (n + chunks - 1) / chunks;
+    chunks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_front, dim3(tx, ty, chunks), dim3(256), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
+                       gray_out, mbits, g.W, g.H, g.WW, ithresh);
     return hipGetLastError();
 }
 
-// Rows per band: the band's local parents (BH x (2 CAP + 1) u32) must fit LDS.
+// LDS of one k_band workgroup: run index (2 x BH x WW u64 + 2 x BH x (WW+1)
+// u16) and the band's local parents (BH x (2 CAP + 1) + 1 u32).
+size_t band_lds(const RowGeom& g, int bh)
+{
+    return (size_t)16 * bh * g.WW + ((size_t)bh * (2 * g.CAP + 1) + 1) * 4 + (size_t)4 * bh * (g.WW + 1);
+}
+
+// Rows per band: the largest power of two <= 8 whose LDS fits.
 int band_rows(const RowGeom& g)
 {
-    int bh = 16;
-    while (bh > 1 && (size_t)bh * (2 * g.CAP + 1) * 4 + 16 > 128 * 1024) bh >>= 1;
+    int bh = 8;
+    while (bh > 1 && band_lds(g, bh) > 150 * 1024) bh >>= 1;
     return bh;
 }
 
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s)
 {
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH;
-    const size_t lds = ((size_t)BH * (2 * g.CAP + 1) + 1) * 4;
-    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), lds, s, c, g, BH);
-    if (nb > 1) hipLaunchKernelGGL(k_merge, dim3(nb - 1, n), dim3(64), 0, s, c, g, BH);
+    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH), s, c, g, BH);
+    if (nb > 1)
+        hipLaunchKernelGGL(k_merge, dim3(nb - 1, n), dim3(64), 32 * g.WW + 8 * (g.WW + 1), s, c, g, BH);
     hipLaunchKernelGGL(k_resolve, dim3(g.H, n), dim3(64), 8 * g.WW + 4 * g.CAP + 16, s, c, g);
     hipLaunchKernelGGL(k_area, dim3(g.H, n), dim3(64), 8 * g.WW, s, c, g);
     hipLaunchKernelGGL(k_paint, dim3(g.H, n), dim3(64), 8 * g.WW, s, c, g, min_area2);
     return hipGetLastError();
 }
 
-hipError_t launch_back(const BackArgs& a, int block, hipStream_t s)
+template <int B, int KMAX>
+static void launch_acc_k(const BackArgs& a, hipStream_t s)
 {
+    const int items = (B + a.ksize - 1) * (B + 2), kit = (items + 63) / 64;
+    dim3 grid((a.g.W + 64 * B - 1) / (64 * B), a.g.H / B);
+    if (kit <= 1) hipLaunchKernelGGL((k_acc<B, 1, KMAX>), grid, dim3(64), 0, s, a);
+    else if (kit <= 2) hipLaunchKernelGGL((k_acc<B, 2, KMAX>), grid, dim3(64), 0, s, a);
+    else if (kit <= 4) hipLaunchKernelGGL((k_acc<B, 4, KMAX>), grid, dim3(64), 0, s, a);
+    else if (kit <= 8) hipLaunchKernelGGL((k_acc<B, 8, KMAX>), grid, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((k_acc<B, 16, KMAX>), grid, dim3(64), 0, s, a);
+}
+
+// small-kernel instantiations keep k_acc's LDS (long-lived workgroups) small,
+// so the contour-filter kernels of the next batch still fit beside it
+template <int B>
+static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
+{
+    if (a.ksize <= 11) launch_acc_k<B, 11>(a, s);
+    else launch_acc_k<B, 63>(a, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t mid)
+{
+    hipError_t e = block == 4 ? launch_acc<4>(a, s) : launch_acc<8>(a, s);
+    if (e != hipSuccess) return e;
+    if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
+    if (!a.overlay && !a.compressed) return hipSuccess;
     if (block == 4) {
-        dim3 grid((a.g.W + 255) / 256, (a.g.H + 15) / 16);
-        hipLaunchKernelGGL(k_back<4>, grid, dim3(256), 0, s, a);
+        dim3 grid((a.g.W + 255) / 256, (a.g.H + 15) / 16, a.n);
+        hipLaunchKernelGGL(k_out<4>, grid, dim3(256), 0, s, a);
     } else {
-        dim3 grid((a.g.W + 511) / 512, (a.g.H + 31) / 32);
-        hipLaunchKernelGGL(k_back<8>, grid, dim3(256), 0, s, a);
+        dim3 grid((a.g.W + 511) / 512, (a.g.H + 31) / 32, a.n);
+        hipLaunchKernelGGL(k_out<8>, grid, dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }

@@ -166,7 +166,8 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out);
 int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* host_dst);
 
 /* With DVC_FLAG_KTIMING: total milliseconds and launch count of the dominant
- * kernel (k_back, one launch per batch) since the last reset (synchronises the handle). reset!=0 clears. */
+ * HBM-bound kernel (k_out: overlay + compress, one launch per batch) since the
+ * last reset (synchronises the handle). reset!=0 clears. */
 int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
 
 void dvc_fd_destroy(dvc_fd* h);
