@@ -18,8 +18,8 @@ per frame instead).
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (k_back: hipEvent time
-per launch on the feed's stream, in a second pass of the same steps) and
+Extra JSON fields: ``roofline`` for the dominant kernel (k_out: hipEvent time
+per launch on the back stream, in a second pass of the same steps) and
 ``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
 feed; rank 0 at N=1 only).
 """
@@ -36,10 +36,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/s (frames/s × H×W) 1080p frame-diff path @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# k_back algorithmic bytes: per frame read BGR 3 + kept-mask 1/8, write overlay 3 + compressed 3;
-# per launch (batch) read + write the accumulated mask once (1 + 1)
+# k_out (the dominant HBM kernel) algorithmic bytes per pixel per frame: read BGR 3 +
+# acc>127 bit 1/8 (+ one static bit per block, negligible), write overlay 3 + compressed 3
 BACK_BYTES_PER_PX_FRAME = 9.125
-BACK_BYTES_PER_PX_LAUNCH = 2
+BACK_BYTES_PER_PX_LAUNCH = 0
 PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 read, new gray 1 written
 
 
@@ -159,7 +159,7 @@ def main():
     st = w.stats()
     w.close()
 
-    # dominant kernel: hipEvent-timed k_back launches (on the back stream), same steps
+    # dominant kernel: hipEvent-timed k_out launches (on the back stream), same steps
     wk = make_worker(ktiming=True)
     run_steps(wk, 1)
     wk.ktime(reset=True)
@@ -184,7 +184,7 @@ def main():
         avg_ms = kms / max(kn, 1)
         bytes_per_launch = (BACK_BYTES_PER_PX_FRAME * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_back")
+        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out")
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -206,7 +206,7 @@ def main():
                        "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
                        "pipeline_bytes_per_px": PIPE_BYTES_PER_PX,
                        "pipeline_GBps_per_gpu": round(PIPE_BYTES_PER_PX * args.steps * P * W * H / elapsed_max / 1e9, 1)},
-            "roofline": {"bound": "hbm", "kernel": "k_back", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_out", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "frames_per_launch": round(kframes / max(kn, 1), 2),
