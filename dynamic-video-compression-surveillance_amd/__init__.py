@@ -1,7 +1,8 @@
 """dvc_amd — MI355X-native per-frame worker for dynamic surveillance compression.
 
 Drop-in for the hot path of carlozamu/dynamic-video-compression-surveillance:
-the frame-differencing worker (``frame_differencing.py``) runs as hand-written
+the frame-differencing worker (``frame_differencing.py``) and the optical-flow
+worker (``motion_compression_opt.py``) run as hand-written
 HIP kernels for gfx950 behind the C-ABI in ``include/dvc.h``; this package is
 the Python host that keeps the reference's function signatures.
 
@@ -12,3 +13,4 @@ __version__ = "0.1.0"
 
 from . import _native  # noqa: F401  (loading is lazy; no CPU fallback)
 from .fd import FDWorker, derive_params  # noqa: F401
+from .of import OFWorker, derive_of_params  # noqa: F401,E402

@@ -16,8 +16,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
-SOURCES = ["fd_kernels.hip", "fd_api.hip"]
-HEADERS = ["fd_kernels.h", "dvc_device.h"]
+SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip"]
+HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 DVC_OK = 0
@@ -26,14 +26,18 @@ DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
 
 PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
+OF_PLANE_RAW, OF_PLANE_SMOOTH, OF_PLANE_MORPH, OF_PLANE_RECT, OF_PLANE_GRAY = range(5)
 
 # every symbol include/dvc.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "dvc_abi_version", "dvc_last_error", "dvc_device_count", "dvc_fd_create", "dvc_fd_prime",
     "dvc_fd_step", "dvc_fd_sync", "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime",
     "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter", "dvc_fd_step_batch",
+    "dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync", "dvc_of_get_stats",
+    "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
+    "dvc_of_debug_read",
 ]
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_BATCH = 512
 
 
@@ -72,6 +76,30 @@ class FdStats(ctypes.Structure):
         ("components", ctypes.c_uint64),
         ("static_blocks", ctypes.c_uint64),
     ]
+
+
+class OfParams(ctypes.Structure):
+    """``dvc_of_params`` (include/dvc.h)."""
+    _fields_ = [
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("flow_threshold", ctypes.c_float),
+        ("quant", ctypes.c_float),
+        ("alpha_fraction", ctypes.c_double),
+        ("window", ctypes.c_int32),
+        ("morph_kernel", ctypes.c_int32),
+        ("pyr_scale", ctypes.c_double),
+        ("levels", ctypes.c_int32),
+        ("winsize", ctypes.c_int32),
+        ("iterations", ctypes.c_int32),
+        ("poly_n", ctypes.c_int32),
+        ("poly_sigma", ctypes.c_double),
+        ("flags", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
+    ]
+
+
+OfStats = FdStats   # same four counters (dvc_of_stats)
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -131,6 +159,26 @@ def lib() -> ctypes.CDLL:
                                     ctypes.c_size_t]
     L.dvc_contour_filter.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int, u8p,
                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.dvc_of_create.argtypes = [ctypes.POINTER(OfParams), ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.dvc_of_prime.argtypes = [vp, u8p, ctypes.c_size_t]
+    L.dvc_of_step.argtypes = [vp, u8p, ctypes.c_size_t, u8p, u8p]
+    L.dvc_of_step_batch.argtypes = [vp, u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, u8p, ctypes.c_size_t,
+                                    u8p, ctypes.c_size_t]
+    L.dvc_of_sync.argtypes = [vp]
+    L.dvc_of_get_stats.argtypes = [vp, ctypes.POINTER(OfStats)]
+    L.dvc_of_read_plane.argtypes = [vp, ctypes.c_int, u8p]
+    L.dvc_of_read_flow.argtypes = [vp, vp]
+    L.dvc_of_ktime.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.dvc_of_destroy.argtypes = [vp]
+    L.dvc_of_debug_read.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int)]
+    L.dvc_of_debug_read.restype = ctypes.c_int
+    L.dvc_of_destroy.restype = None
+    L.dvc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                  u8p]
+    for name in ("dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync",
+                 "dvc_of_get_stats", "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_compress"):
+        getattr(L, name).restype = ctypes.c_int
     for name in ("dvc_device_count", "dvc_fd_create", "dvc_fd_prime", "dvc_fd_step", "dvc_fd_sync",
                  "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime", "dvc_gaussian_taps_q8",
                  "dvc_contour_filter", "dvc_fd_step_batch"):
@@ -157,6 +205,20 @@ def contour_filter(mask, min_area2: int, device: int = 0):
     check(lib().dvc_contour_filter(m.ctypes.data, W, H, int(min_area2), int(device), out.ctypes.data,
                                    ctypes.byref(nc)))
     return out, int(nc.value)
+
+
+def of_compress(bgr, mask, quant: float = 100.0, device: int = 0):
+    """compress_with_motion for one frame with an arbitrary mask (of:151-183) on the GPU."""
+    import numpy as np
+    f = np.ascontiguousarray(bgr, dtype=np.uint8)
+    m = np.ascontiguousarray(mask, dtype=np.uint8)
+    H, W = m.shape
+    if f.shape != (H, W, 3):
+        raise ValueError("frame and mask shapes differ")
+    out = np.empty_like(f)
+    check(lib().dvc_of_compress(f.ctypes.data, 3 * W, m.ctypes.data, W, H, float(quant), int(device),
+                                out.ctypes.data))
+    return out
 
 
 def gaussian_taps_q8(n: int, sigma: float) -> list:

@@ -16,8 +16,9 @@
 
 #include "../../include/dvc.h"
 #include "fd_kernels.h"
+#include "host_common.h"
 
-namespace {
+namespace dvc_host {
 
 thread_local std::string g_err;
 
@@ -32,20 +33,14 @@ int fail(int code, const char* fmt, ...)
     return code;
 }
 
-#define HIP_OK(expr)                                                                          \
-    do {                                                                                      \
-        hipError_t e_ = (expr);                                                               \
-        if (e_ != hipSuccess)                                                                 \
-            return fail(DVC_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
-                        __FILE__, __LINE__);                                                  \
-    } while (0)
+const char* last_error() { return g_err.c_str(); }
 
-// getGaussianKernelBitExact + getGaussianKernelFixedPoint_ED (8 fraction bits):
-// the taps OpenCV's 8U GaussianBlur uses (fd:77, fd:93).
-int gauss_taps(int n, double sigma, uint16_t* taps)
+// getGaussianKernelBitExact in double (OpenCV 4.11): the small binomial tables
+// for sigma <= 0 and n <= 7, else exp(-x^2 / 2 sigma^2) normalised with the
+// centre tap 1/sum. The float kernels of getGaussianKernel(CV_32F) are these
+// values cast to float.
+void gauss_f64(int n, double sigma, double* k)
 {
-    if (n < 1 || n > 63 || (n & 1) == 0) return -1;
-    double k[64];
     if (sigma <= 0 && n <= 7) {
         static const double t1[] = {1.0};
         static const double t3[] = {0.25, 0.5, 0.25};
@@ -53,20 +48,46 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
         static const double t7[] = {0.03125, 0.109375, 0.21875, 0.28125, 0.21875, 0.109375, 0.03125};
         const double* t = n == 1 ? t1 : n == 3 ? t3 : n == 5 ? t5 : t7;
         for (int i = 0; i < n; ++i) k[i] = t[i];
-    } else {
-        double sx = sigma > 0 ? sigma : std::fma((double)n, 0.15, 0.35);
-        double scale2X = -0.125 / (sx * sx);
-        int n2 = (n - 1) / 2;
-        double vals[32], sum = 0.0;
-        for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
-            vals[i] = std::exp((double)(x * x) * scale2X);
-            sum += vals[i];
-        }
-        sum = sum * 2.0 + 1.0;
-        double mul1 = 1.0 / sum;
-        for (int i = 0; i < n2; ++i) k[i] = k[n - 1 - i] = vals[i] * mul1;
-        k[n2] = mul1;
+        return;
     }
+    double sx = sigma > 0 ? sigma : std::fma((double)n, 0.15, 0.35);
+    double scale2X = -0.125 / (sx * sx);
+    int n2 = (n - 1) / 2;
+    double vals[64], sum = 0.0;
+    for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
+        vals[i] = std::exp((double)(x * x) * scale2X);
+        sum += vals[i];
+    }
+    sum = sum * 2.0 + 1.0;
+    double mul1 = 1.0 / sum;
+    for (int i = 0; i < n2; ++i) k[i] = k[n - 1 - i] = vals[i] * mul1;
+    k[n2] = mul1;
+}
+
+void dct_matrix(int B, float* M)
+{
+    const double PI = 3.14159265358979323846;
+    for (int k = 0; k < B; ++k)
+        for (int n = 0; n < B; ++n) {
+            double c = k == 0 ? std::sqrt(1.0 / B) : std::sqrt(2.0 / B);
+            M[k * B + n] = (float)(c * std::cos(PI * (2 * n + 1) * k / (2.0 * B)));
+        }
+}
+
+}  // namespace dvc_host
+
+namespace {
+
+using dvc_host::fail;
+using dvc_host::dct_matrix;
+
+// getGaussianKernelBitExact + getGaussianKernelFixedPoint_ED (8 fraction bits):
+// the taps OpenCV's 8U GaussianBlur uses (fd:77, fd:93).
+int gauss_taps(int n, double sigma, uint16_t* taps)
+{
+    if (n < 1 || n > 63 || (n & 1) == 0) return -1;
+    double k[64];
+    dvc_host::gauss_f64(n, sigma, k);
     int n2 = n / 2;
     double err = 0.0;
     long long s = 0;
@@ -79,16 +100,6 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
     }
     taps[n2] = (uint16_t)(256 - 2 * s);
     return 0;
-}
-
-void dct_matrix(int B, float* M)
-{
-    const double PI = 3.14159265358979323846;
-    for (int k = 0; k < B; ++k)
-        for (int n = 0; n < B; ++n) {
-            double c = k == 0 ? std::sqrt(1.0 / B) : std::sqrt(2.0 / B);
-            M[k * B + n] = (float)(c * std::cos(PI * (2 * n + 1) * k / (2.0 * B)));
-        }
 }
 
 }  // namespace
@@ -172,7 +183,7 @@ extern "C" {
 
 int dvc_abi_version(void) { return DVC_ABI_VERSION; }
 
-const char* dvc_last_error(void) { return g_err.c_str(); }
+const char* dvc_last_error(void) { return dvc_host::last_error(); }
 
 int dvc_device_count(int* count)
 {

@@ -1,0 +1,612 @@
+// of_api.hip — the C-ABI (include/dvc.h, dvc_of_*) of the optical-flow worker.
+//
+// Host side of one camera feed of motion_compression_opt.py: the state the
+// reference keeps in Python locals (prev_gray of:60,101; mask_queue of:61,84)
+// lives on the device as per-level polynomial-expansion rings, the raw-mask
+// ring and the per-pixel vote counts. The per-level geometry (pyramid sizes,
+// smoothing kernels, INTER_LINEAR tables, FarnebackPrepareGaussian) is derived
+// here with the same expressions as oracle/of_oracle.c.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <algorithm>
+#include <vector>
+
+#include "../../include/dvc.h"
+#include "host_common.h"
+#include "of_kernels.h"
+
+using dvc_host::fail;
+
+namespace {
+
+// FarnebackPrepareGaussian (optflowgf.cpp; oc_poly_gauss): float taps, and the
+// needed entries of the inverse moment matrix (Cholesky, double).
+void poly_coef(int n, double sigma, dvc::PolyCoef& pc)
+{
+    float g[2 * dvc::OF_MAX_POLY_N + 1], xg[2 * dvc::OF_MAX_POLY_N + 1], xxg[2 * dvc::OF_MAX_POLY_N + 1];
+    if (sigma < FLT_EPSILON) sigma = n * 0.3;
+    double s = 0.;
+    for (int x = -n; x <= n; ++x) {
+        g[x + n] = (float)std::exp(-x * x / (2 * sigma * sigma));
+        s += g[x + n];
+    }
+    s = 1. / s;
+    for (int x = -n; x <= n; ++x) {
+        g[x + n] = (float)(g[x + n] * s);
+        xg[x + n] = (float)(x * g[x + n]);
+        xxg[x + n] = (float)(x * x * g[x + n]);
+    }
+    double G[6][6];
+    std::memset(G, 0, sizeof(G));
+    for (int y = -n; y <= n; ++y)
+        for (int x = -n; x <= n; ++x) {
+            G[0][0] += g[y + n] * g[x + n];
+            G[1][1] += g[y + n] * g[x + n] * x * x;
+            G[3][3] += g[y + n] * g[x + n] * x * x * x * x;
+            G[5][5] += g[y + n] * g[x + n] * x * x * y * y;
+        }
+    G[2][2] = G[0][3] = G[0][4] = G[3][0] = G[4][0] = G[1][1];
+    G[4][4] = G[3][3];
+    G[3][4] = G[4][3] = G[5][5];
+    double L[6][6];
+    std::memset(L, 0, sizeof(L));
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double v = G[i][j];
+            for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
+            L[i][j] = (i == j) ? std::sqrt(v) : v / L[j][j];
+        }
+    double inv[6][6];
+    for (int c = 0; c < 6; ++c) {
+        double z[6], xv[6];
+        for (int i = 0; i < 6; ++i) {
+            double v = (i == c) ? 1.0 : 0.0;
+            for (int k = 0; k < i; ++k) v -= L[i][k] * z[k];
+            z[i] = v / L[i][i];
+        }
+        for (int i = 5; i >= 0; --i) {
+            double v = z[i];
+            for (int k = i + 1; k < 6; ++k) v -= L[k][i] * xv[k];
+            xv[i] = v / L[i][i];
+        }
+        for (int i = 0; i < 6; ++i) inv[i][c] = xv[i];
+    }
+    pc.n = n;
+    for (int i = 0; i < 2 * n + 1; ++i) {
+        pc.g[i] = g[i];
+        pc.xg[i] = xg[i];
+        pc.xxg[i] = xxg[i];
+    }
+    pc.ig11 = inv[1][1];
+    pc.ig03 = inv[0][3];
+    pc.ig33 = inv[3][3];
+    pc.ig55 = inv[5][5];
+}
+
+// INTER_LINEAR source taps of a resize sw -> dw (oc_resize_linear_f32, one axis).
+void lin_taps(int sw, int dw, std::vector<dvc::LinTap>& out)
+{
+    out.resize(dw);
+    const double sc = (double)sw / dw;
+    for (int d = 0; d < dw; ++d) {
+        float f = (float)((d + 0.5) * sc - 0.5);
+        int s = (int)std::floor(f);
+        f -= (float)s;
+        if (s < 0) { f = 0.f; s = 0; }
+        if (s >= sw - 1) { f = 0.f; s = sw - 1; }
+        const int s1 = s + 1 < sw ? s + 1 : sw - 1;
+        out[d] = dvc::LinTap{s, s1, 1.f - f, f};
+    }
+}
+
+// smallest c with c*255 >= alpha*L*255 in float64 (of:86; oc_vote_threshold)
+int vote_threshold(double alpha, int L)
+{
+    const double thr = alpha * L * 255;
+    int c = 0;
+    while (c <= L && !((double)(c * 255) >= thr)) ++c;
+    return c;
+}
+
+}  // namespace
+
+struct dvc_of {
+    dvc_of_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    dvc::OfGeom g{};
+    dvc::Level lv[dvc::OF_MAX_LEVELS]{};
+    dvc::OfBufs b{};
+    dvc::DctMat M{};
+    int max_batch = 1;
+    long long a_next = 1;
+    bool primed = false;
+    uint64_t frames = 0;
+    int last_n = 0;
+    std::vector<void*> dev;  // every device allocation
+    uint8_t *d_in = nullptr, *d_mask = nullptr, *d_cp = nullptr;
+    uint8_t *h_in = nullptr, *h_mask = nullptr, *h_cp = nullptr;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+};
+
+static void of_free(dvc_of* h)
+{
+    for (void* p : h->dev)
+        if (p) (void)hipFree(p);
+    h->dev.clear();
+    for (void* p : {(void*)h->h_in, (void*)h->h_mask, (void*)h->h_cp})
+        if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+template <typename T>
+static hipError_t of_alloc(dvc_of* h, T** p, size_t bytes)
+{
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+    if (e == hipSuccess) {
+        h->dev.push_back(q);
+        *p = reinterpret_cast<T*>(q);
+    }
+    return e;
+}
+
+extern "C" {
+
+int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of** out)
+{
+    if (!prm || !out) return fail(DVC_E_INVALID, "NULL argument");
+    const dvc_of_params& p = *prm;
+    if (p.width < 8 || p.height < 8 || p.width > 65520)
+        return fail(DVC_E_INVALID, "frame %dx%d outside 8..65520 x >=8", p.width, p.height);
+    if (p.width % 8 || p.height % 8)
+        return fail(DVC_E_UNSUPPORTED, "frame %dx%d: the GPU path needs multiples of 8", p.width, p.height);
+    if (p.morph_kernel != 2) return fail(DVC_E_UNSUPPORTED, "morph_kernel %d: the GPU path implements 2", p.morph_kernel);
+    if (p.window < 1 || p.window > 127) return fail(DVC_E_UNSUPPORTED, "window_size %d outside 1..127", p.window);
+    if (p.poly_n != 5 && p.poly_n != 7) return fail(DVC_E_UNSUPPORTED, "poly_n %d: 5 or 7", p.poly_n);
+    if (p.winsize < 1 || p.winsize / 2 > dvc::OF_MAX_BOX_M)
+        return fail(DVC_E_UNSUPPORTED, "winsize %d outside 1..%d", p.winsize, 2 * dvc::OF_MAX_BOX_M + 1);
+    if (p.iterations < 1) return fail(DVC_E_INVALID, "iterations must be >= 1");
+    if (!(p.pyr_scale > 0 && p.pyr_scale < 1)) return fail(DVC_E_INVALID, "pyr_scale must be in (0, 1)");
+    if (p.levels < 0) return fail(DVC_E_INVALID, "levels must be >= 0");
+    if (!(p.quant == p.quant) || p.quant == 0.0f) return fail(DVC_E_INVALID, "quant must be nonzero");
+    if (p.max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %u outside 1..%d", p.max_batch, DVC_MAX_BATCH);
+    // pyramid depth (oc_fb_levels: min size 32)
+    int L = 0;
+    {
+        double scale = 1;
+        for (L = 0; L < p.levels; ++L) {
+            scale *= p.pyr_scale;
+            if (p.width * scale < 32 || p.height * scale < 32) break;
+        }
+    }
+    if (L >= dvc::OF_MAX_LEVELS) return fail(DVC_E_UNSUPPORTED, "%d pyramid levels (max %d)", L + 1, dvc::OF_MAX_LEVELS);
+
+    dvc_of* h = new dvc_of();
+    h->p = p;
+    h->device = device;
+    h->max_batch = p.max_batch == 0 ? 1 : (int)p.max_batch;
+    const int mb = h->max_batch;
+    dvc::OfGeom& g = h->g;
+    g.W = p.width;
+    g.H = p.height;
+    g.WW = (p.width + 63) / 64;
+    g.CAP = p.width / 2 + 1;
+    g.L = L;
+    g.RS = mb + 1;
+    g.RB = p.window + mb;
+    g.iters = p.iterations;
+    g.m = p.winsize / 2;
+    g.box_scale = 1. / (p.winsize * p.winsize);
+    g.up = (float)(1. / p.pyr_scale);
+    g.flow_thr = p.flow_threshold;
+    poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
+    dvc_host::dct_matrix(8, h->M.m);
+
+    auto bad = [&](hipError_t e, const char* what) {
+        int rc = fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "%s: %s", what, hipGetErrorString(e));
+        of_free(h);
+        delete h;
+        return rc;
+    };
+    auto unsupported = [&](const char* what, int v) {
+        int rc = fail(DVC_E_UNSUPPORTED, what, v);
+        of_free(h);
+        delete h;
+        return rc;
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return bad(e, "hipSetDevice");
+    if (hip_stream) {
+        h->stream = (hipStream_t)hip_stream;
+    } else {
+        if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+        h->own_stream = true;
+    }
+    const size_t W = p.width, H = p.height, N = W * H, WW = g.WW, CAP = g.CAP;
+    // levels (oc_fb_level_poly geometry)
+    std::vector<dvc::LinTap> tabs;   // all tables, uploaded once
+    struct TabRef { size_t xt, yt, ux, uy; } tr[dvc::OF_MAX_LEVELS];
+    for (int k = 0; k <= L; ++k) {
+        dvc::Level& lv = h->lv[k];
+        double scale = 1;
+        for (int i = 0; i < k; ++i) scale *= p.pyr_scale;
+        const double sigma = (1. / scale - 1) * 0.5;
+        int sz = ((int)std::lrint(sigma * 5)) | 1;
+        if (sz < 3) sz = 3;
+        if (sz > dvc::OF_MAX_BLUR) return unsupported("pyramid smoothing kernel of %d taps (max 63)", sz);
+        lv.w = (int)std::lrint(p.width * scale);
+        lv.h = (int)std::lrint(p.height * scale);
+        lv.r = sz / 2;
+        double kd[64];
+        dvc_host::gauss_f64(sz, sigma, kd);
+        for (int i = 0; i < sz; ++i) lv.kf[i] = (float)kd[i];
+        std::vector<dvc::LinTap> t;
+        tr[k].xt = tabs.size();
+        lin_taps(p.width, lv.w, t);
+        tabs.insert(tabs.end(), t.begin(), t.end());
+        tr[k].yt = tabs.size();
+        lin_taps(p.height, lv.h, t);
+        tabs.insert(tabs.end(), t.begin(), t.end());
+        tr[k].ux = tr[k].uy = 0;
+    }
+    for (int k = 0; k < L; ++k) {
+        std::vector<dvc::LinTap> t;
+        tr[k].ux = tabs.size();
+        lin_taps(h->lv[k + 1].w, h->lv[k].w, t);
+        tabs.insert(tabs.end(), t.begin(), t.end());
+        tr[k].uy = tabs.size();
+        lin_taps(h->lv[k + 1].h, h->lv[k].h, t);
+        tabs.insert(tabs.end(), t.begin(), t.end());
+    }
+    dvc::LinTap* dtab = nullptr;
+    if ((e = of_alloc(h, &dtab, sizeof(dvc::LinTap) * tabs.size())) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemcpy(dtab, tabs.data(), sizeof(dvc::LinTap) * tabs.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return bad(e, "hipMemcpy");
+    for (int k = 0; k <= L; ++k) {
+        dvc::Level& lv = h->lv[k];
+        const size_t px = (size_t)lv.w * lv.h;
+        lv.xt = dtab + tr[k].xt;
+        lv.yt = dtab + tr[k].yt;
+        lv.ux = k < L ? dtab + tr[k].ux : nullptr;
+        lv.uy = k < L ? dtab + tr[k].uy : nullptr;
+        if ((e = of_alloc(h, &lv.R, 20 * px * g.RS)) != hipSuccess) return bad(e, "hipMalloc");
+        for (int q = 0; q < 2; ++q)
+            if ((e = of_alloc(h, &lv.flow[q], 8 * px * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if (k > 0 && (e = of_alloc(h, &lv.tmpc, 4 * H * 2 * (size_t)lv.w * mb)) != hipSuccess) return bad(e, "hipMalloc");
+    }
+    dvc::OfBufs& b = h->b;
+    struct { void** ptr; size_t bytes; } allocs[] = {
+        {(void**)&b.gray, N * mb},
+        {(void**)&b.mring, 8 * H * WW * g.RB},
+        {(void**)&b.cnt, 64 * H * WW},
+        {(void**)&b.vthr, 256},
+        {(void**)&b.sbits, 8 * H * WW * mb},
+        {(void**)&b.obits, 8 * H * WW * mb},
+        {(void**)&b.rbits, 8 * H * WW * mb},
+        {(void**)&b.rs, 2 * H * CAP * mb},
+        {(void**)&b.re, 2 * H * CAP * mb},
+        {(void**)&b.nfg, 4 * H * mb},
+        {(void**)&b.fpar, 4 * H * CAP * mb},
+        {(void**)&b.bx0, 4 * H * CAP * mb},
+        {(void**)&b.bx1, 4 * H * CAP * mb},
+        {(void**)&b.by0, 4 * H * CAP * mb},
+        {(void**)&b.by1, 4 * H * CAP * mb},
+        {(void**)&b.roots, 4 * H * CAP * mb},
+        {(void**)&b.nroots, 4 * (size_t)mb},
+        {(void**)&b.stats, 8 * 4 * 64},
+    };
+    for (auto& a : allocs)
+        if ((e = of_alloc(h, a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
+    if (p.flags & DVC_FLAG_KEEP_PLANES)
+        if ((e = of_alloc(h, &b.dbg_flow, 8 * N)) != hipSuccess) return bad(e, "hipMalloc");
+    uint8_t vt[256];
+    std::memset(vt, 0, sizeof(vt));
+    for (int l = 1; l <= p.window; ++l) vt[l] = (uint8_t)vote_threshold(p.alpha_fraction, l);
+    if ((e = hipMemcpy((void*)b.vthr, vt, 256, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+    if (!(p.flags & DVC_FLAG_DEVICE_PTRS)) {
+        if ((e = of_alloc(h, &h->d_in, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = of_alloc(h, &h->d_mask, N * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = of_alloc(h, &h->d_cp, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_in, 3 * N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_mask, N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_cp, 3 * N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
+    }
+    if ((e = hipMemsetAsync(b.stats, 0, 8 * 4 * 64, h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return bad(e, "hipStreamSynchronize");
+    *out = h;
+    return DVC_OK;
+}
+
+int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
+{
+    if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
+    if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
+    const uint8_t* d = bgr;
+    int dp = (int)pitch;
+    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
+        for (size_t y = 0; y < H; ++y) std::memcpy(h->h_in + y * 3 * W, bgr + y * pitch, 3 * W);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, 3 * N, hipMemcpyHostToDevice, h->stream));
+        d = h->d_in;
+        dp = (int)(3 * W);
+    }
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, 3 * N, 0, 1, h->stream));   // of:60
+    HIP_OK(hipMemsetAsync(h->b.mring, 0, 8 * H * WW * h->g.RB, h->stream));            // of:61 deque()
+    HIP_OK(hipMemsetAsync(h->b.cnt, 0, 64 * H * WW, h->stream));
+    HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    h->a_next = 1;
+    h->frames = 0;
+    h->last_n = 0;
+    h->primed = true;
+    return DVC_OK;
+}
+
+}  // extern "C"
+
+static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* mask, size_t mstride,
+                      uint8_t* cp, size_t ostride)
+{
+    const long long a0 = h->a_next;
+    const bool timed = h->p.flags & DVC_FLAG_KTIMING;
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->stream));
+    if (timed) {
+        while (h->ev.size() < h->ev_used + 2) {
+            hipEvent_t e;
+            HIP_OK(hipEventCreate(&e));
+            h->ev.push_back(e);
+        }
+    }
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->stream));
+    if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->stream));
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->stream));
+    if (timed) {
+        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->stream));
+        h->ev_used += 2;
+    }
+    HIP_OK(dvc::of_launch_mask(h->g, h->b, a0, h->p.window, n, h->stream));
+    dvc::OfOutArgs o{};
+    o.bgr = d;
+    o.pitch = dp;
+    o.fstride = fstride;
+    o.mask = mask;
+    o.mstride = mstride;
+    o.compressed = cp;
+    o.ostride = ostride;
+    o.quant = h->p.quant;
+    o.M = h->M;
+    HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->stream));
+    h->a_next += n;
+    h->frames += (uint64_t)n;
+    h->last_n = n;
+    return DVC_OK;
+}
+
+static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, int n, uint8_t* mask, size_t mstride,
+                  uint8_t* compressed, size_t ostride)
+{
+    if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
+    if (!h->primed) return fail(DVC_E_STATE, "step before dvc_of_prime");
+    if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
+    const size_t W = h->p.width, H = h->p.height, N = W * H, row = 3 * W;
+    if (pitch < row || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (n > 1 && (fstride < pitch * (H - 1) + row || fstride % 4))
+        return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
+    if (n > 1 && mask && (mstride < N || mstride % 8)) return fail(DVC_E_INVALID, "mask stride %zu invalid", mstride);
+    if (n > 1 && compressed && (ostride < 3 * N || ostride % 4))
+        return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
+    HIP_OK(hipSetDevice(h->device));
+    const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
+    for (int f0 = 0; f0 < n; f0 += h->max_batch) {
+        const int m = std::min(h->max_batch, n - f0);
+        const uint8_t* in = bgr + (size_t)f0 * fstride;
+        uint8_t* mk = mask ? mask + (size_t)f0 * mstride : nullptr;
+        uint8_t* cp = compressed ? compressed + (size_t)f0 * ostride : nullptr;
+        if (devp) {
+            int rc = of_enqueue(h, in, (int)pitch, fstride, m, mk, mstride, cp, ostride);
+            if (rc) return rc;
+            continue;
+        }
+        for (int t = 0; t < m; ++t)
+            for (size_t y = 0; y < H; ++y)
+                std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->stream));
+        int rc = of_enqueue(h, h->d_in, (int)row, 3 * N, m, mk ? h->d_mask : nullptr, N, cp ? h->d_cp : nullptr, 3 * N);
+        if (rc) return rc;
+        if (mk) HIP_OK(hipMemcpyAsync(h->h_mask, h->d_mask, (size_t)m * N, hipMemcpyDeviceToHost, h->stream));
+        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->stream));
+        HIP_OK(hipStreamSynchronize(h->stream));
+        for (int t = 0; t < m; ++t) {
+            if (mk) std::memcpy(mk + (size_t)t * mstride, h->h_mask + (size_t)t * N, N);
+            if (cp) std::memcpy(cp + (size_t)t * ostride, h->h_cp + (size_t)t * 3 * N, 3 * N);
+        }
+    }
+    return DVC_OK;
+}
+
+extern "C" {
+
+int dvc_of_step(dvc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_t* compressed)
+{
+    return of_run(h, bgr, pitch, 0, 1, mask, 0, compressed, 0);
+}
+
+int dvc_of_step_batch(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, int n, uint8_t* mask,
+                      size_t mask_stride, uint8_t* compressed, size_t out_stride)
+{
+    return of_run(h, bgr, pitch, frame_stride, n, mask, mask_stride, compressed, out_stride);
+}
+
+int dvc_of_sync(dvc_of* h)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    return DVC_OK;
+}
+
+int dvc_of_get_stats(dvc_of* h, dvc_of_stats* out)
+{
+    if (!h || !out) return fail(DVC_E_INVALID, "NULL argument");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    unsigned long long slots[64 * 4], s[4] = {0, 0, 0, 0};
+    HIP_OK(hipMemcpy(slots, h->b.stats, sizeof(slots), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 64 * 4; ++i) s[i % 4] += slots[i];
+    out->frames = h->frames;
+    out->motion_px = s[1];
+    out->components = s[2];
+    out->static_blocks = s[3];
+    return DVC_OK;
+}
+
+int dvc_of_read_plane(dvc_of* h, int plane, uint8_t* dst)
+{
+    if (!h || !dst) return fail(DVC_E_INVALID, "NULL argument");
+    if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW, t = (size_t)h->last_n - 1;
+    if (plane == DVC_OF_PLANE_GRAY) {
+        HIP_OK(hipMemcpy(dst, h->b.gray + t * N, N, hipMemcpyDeviceToHost));
+        return DVC_OK;
+    }
+    const uint64_t* src = nullptr;
+    switch (plane) {
+    case DVC_OF_PLANE_RAW: src = h->b.mring + (size_t)((h->a_next - 1) % h->g.RB) * H * WW; break;
+    case DVC_OF_PLANE_SMOOTH: src = h->b.sbits + t * H * WW; break;
+    case DVC_OF_PLANE_MORPH: src = h->b.obits + t * H * WW; break;
+    case DVC_OF_PLANE_RECT: src = h->b.rbits + t * H * WW; break;
+    default: return fail(DVC_E_INVALID, "unknown plane %d", plane);
+    }
+    std::vector<uint64_t> bits(H * WW);
+    HIP_OK(hipMemcpy(bits.data(), src, 8 * H * WW, hipMemcpyDeviceToHost));
+    for (size_t y = 0; y < H; ++y)
+        for (size_t x = 0; x < W; ++x) dst[y * W + x] = ((bits[y * WW + x / 64] >> (x % 64)) & 1) ? 255 : 0;
+    return DVC_OK;
+}
+
+int dvc_of_read_flow(dvc_of* h, float* dst)
+{
+    if (!h || !dst) return fail(DVC_E_INVALID, "NULL argument");
+    if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
+    if (!h->b.dbg_flow) return fail(DVC_E_STATE, "flow readback needs DVC_FLAG_KEEP_PLANES");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(hipMemcpy(dst, h->b.dbg_flow, 8 * (size_t)h->p.width * h->p.height, hipMemcpyDeviceToHost));
+    return DVC_OK;
+}
+
+int dvc_of_ktime(dvc_of* h, double* total_ms, uint64_t* launches, int reset)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    double t = 0.0;
+    for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (h->ev_used / 2) * (uint64_t)h->g.iters;
+    if (reset) h->ev_used = 0;
+    return DVC_OK;
+}
+
+int dvc_of_debug_read(dvc_of* h, int what, int level, void* dst, int* w, int* hgt)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    if (level < 0 || level > h->g.L) return fail(DVC_E_INVALID, "level %d outside 0..%d", level, h->g.L);
+    const dvc::Level& L = h->lv[level];
+    if (w) *w = L.w;
+    if (hgt) *hgt = L.h;
+    if (!dst) return DVC_OK;
+    if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    const size_t px = (size_t)L.w * L.h;
+    const long long a = h->a_next - 1;
+    const void* src = nullptr;
+    size_t bytes = 0;
+    if (what == 0 || what == 1) {
+        src = L.R + (size_t)(((a - what) % h->g.RS + h->g.RS) % h->g.RS) * px * 5;
+        bytes = 20 * px;
+    } else if (what == 2) {
+        if (level == 0 && h->g.iters < 2) return fail(DVC_E_STATE, "level 0 keeps no flow with 1 iteration");
+        src = L.flow[0] + (size_t)(h->last_n - 1) * px * 2;
+        bytes = 8 * px;
+    } else {
+        return fail(DVC_E_INVALID, "unknown debug item %d", what);
+    }
+    HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return DVC_OK;
+}
+
+void dvc_of_destroy(dvc_of* h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    of_free(h);
+    delete h;
+}
+
+int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int width, int height, float quant,
+                    int device, uint8_t* out)
+{
+    if (!bgr || !mask || !out) return fail(DVC_E_INVALID, "NULL argument");
+    if (width < 8 || height < 8 || width % 8 || height % 8)
+        return fail(DVC_E_UNSUPPORTED, "frame %dx%d: the GPU path needs multiples of 8", width, height);
+    if (pitch < 3 * (size_t)width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (!(quant == quant) || quant == 0.0f) return fail(DVC_E_INVALID, "quant must be nonzero");
+    HIP_OK(hipSetDevice(device));
+    const size_t W = width, H = height, N = W * H, WW = (W + 63) / 64;
+    std::vector<uint64_t> bits(H * WW, 0);
+    for (size_t y = 0; y < H; ++y)
+        for (size_t x = 0; x < W; ++x)
+            if (mask[y * W + x]) bits[y * WW + x / 64] |= 1ull << (x % 64);
+    std::vector<uint8_t> in(3 * N);
+    for (size_t y = 0; y < H; ++y) std::memcpy(in.data() + y * 3 * W, bgr + y * pitch, 3 * W);
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    uint64_t* d_bits = nullptr;
+    hipError_t e = hipMalloc((void**)&d_in, 3 * N);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_out, 3 * N);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_bits, 8 * H * WW);
+    if (e == hipSuccess) e = hipMemcpy(d_in, in.data(), 3 * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_bits, bits.data(), 8 * H * WW, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        dvc::OfGeom g{};
+        g.W = width;
+        g.H = height;
+        g.WW = (int)WW;
+        dvc::OfBufs b{};
+        b.rbits = d_bits;
+        dvc::OfOutArgs o{};
+        o.bgr = d_in;
+        o.pitch = 3 * width;
+        o.fstride = 3 * N;
+        o.compressed = d_out;
+        o.ostride = 3 * N;
+        o.quant = quant;
+        dvc_host::dct_matrix(8, o.M.m);
+        e = dvc::of_launch_out(g, b, o, 1, nullptr);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, 3 * N, hipMemcpyDeviceToHost);
+    for (void* p : {(void*)d_in, (void*)d_out, (void*)d_bits})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(DVC_E_HIP, "of compress: %s", hipGetErrorString(e));
+    return DVC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,872 @@
+// of_kernels.hip — gfx950 (MI355X / CDNA4) kernels of the optical-flow (OF)
+// per-frame worker (reference: motion_compression_opt.py:65-101, 141-185).
+//
+// One batch of n consecutive frames = these launches (of_kernels.h):
+//   k_of_front0   BGR->gray (of:71), level-0 smoothing (3 taps, sigma 0) and
+//                 FarnebackPolyExp -> R of level 0 (5 floats / px)
+//   k_pyr_h       level k > 0: horizontal Gaussian pass at the source columns
+//                 the INTER_LINEAR resize reads
+//   k_pyr_poly    level k > 0: vertical pass + resize + FarnebackPolyExp
+//   k_flow        per level (coarse to fine) and iteration: the flow of the
+//                 previous iteration (or the upsampled coarser flow) ->
+//                 FarnebackUpdateMatrices over the tile + box halo in LDS ->
+//                 box-filtered G, h (double, direct sums) -> flow = G^-1 h
+//                 (FarnebackUpdateFlow_Blur); the finest level's last
+//                 iteration emits |flow| > thr as bits (of:82-83)
+//   k_vote        sliding 30-frame vote (of:84-86), frames in order per tile
+//   k_of_band     MORPH_CLOSE + MORPH_OPEN with the 2x2 ellipse (of:89-90) on
+//                 a band of rows, then its 8-connected runs + union-find in LDS
+//   k_of_merge    band seams -> global unions
+//   k_of_bbox     bounding box per component (of:93-96), roots compacted
+//   k_of_rect     rectangles (x0..x1+1, y0..y1+1) OR-painted (of:97)
+//   k_of_out      static 8x8 blocks: DCT quantisation of Y, Cr, Cb, YCrCb->BGR,
+//                 BGR->gray->BGR (of:151-183), + the rectangle mask bytes
+//
+// Every float/double expression follows oracle/of_oracle.c operation by
+// operation (compiled with -ffp-contract=off on both sides), so the flow, and
+// with it every mask bit, is identical to the oracle's. No MFMA: nothing here
+// is a dense contraction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "dvc_device.h"
+#include "of_kernels.h"
+
+namespace dvc {
+
+namespace {
+
+constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
+constexpr int FL_W = 64, FL_H = 16;   // flow tile
+
+__device__ __forceinline__ long long ring(long long a, int n) { return ((a % n) + n) % n; }
+
+// ------------------------------------------------- polynomial expansion -----
+// Steps C and D of FarnebackPolyExp (oc_poly_exp) for one tile whose smoothed
+// level image I is in LDS at rows [y0-PN, y0+PT_H-1+PN], cols [x0-PN, ...]
+// (in-image entries only). sv: PT_H x (PT_W+2PN) x 3 floats.
+template <int PN>
+__device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0, int y0, int w, int h,
+                          float* __restrict__ R)
+{
+    constexpr int IW = PT_W + 2 * PN;
+    const int tid = threadIdx.x;
+    // vertical part, float (oc_poly_exp: r = s*g0; t += g_k*(a+b) ...)
+    for (int idx = tid; idx < PT_H * IW; idx += 256) {
+        const int i = idx / IW, j = idx - i * IW;
+        const int y = y0 + i, x = x0 - PN + j;
+        if (y >= h || x < 0 || x >= w) continue;
+        const int li = i + PN;
+        float r0 = sI[li * IW + j] * pc.g[PN];
+        float r1 = 0.f, r2 = 0.f;
+#pragma unroll
+        for (int k = 1; k <= PN; ++k) {
+            const float g0 = pc.g[PN + k], g1 = pc.xg[PN + k], g2 = pc.xxg[PN + k];
+            const int ya = max(y - k, 0) - (y0 - PN), yb = min(y + k, h - 1) - (y0 - PN);
+            const float a = sI[ya * IW + j], b = sI[yb * IW + j];
+            const float p = a + b;
+            const float t0 = r0 + g0 * p;
+            const float t1 = r1 + g1 * (b - a);
+            const float t2 = r2 + g2 * p;
+            r0 = t0;
+            r1 = t1;
+            r2 = t2;
+        }
+        float* v = sv + (i * IW + j) * 3;
+        v[0] = r0;
+        v[1] = r1;
+        v[2] = r2;
+    }
+    __syncthreads();
+    // horizontal part, double; replicated row ends
+    for (int idx = tid; idx < PT_H * PT_W; idx += 256) {
+        const int i = idx / PT_W, jx = idx - i * PT_W;
+        const int y = y0 + i, x = x0 + jx;
+        if (y >= h || x >= w) continue;
+        const float* c = sv + (i * IW + jx + PN) * 3;
+        const double gc = (double)pc.g[PN];
+        double b1 = (double)c[0] * gc, b2 = 0, b3 = (double)c[1] * gc, b4 = 0;
+        double b5 = (double)c[2] * gc, b6 = 0;
+#pragma unroll
+        for (int k = 1; k <= PN; ++k) {
+            const float* P = sv + (i * IW + (min(x + k, w - 1) - (x0 - PN))) * 3;
+            const float* M = sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
+            const double gk = (double)pc.g[PN + k], xgk = (double)pc.xg[PN + k], xxgk = (double)pc.xxg[PN + k];
+            const double tg = (double)P[0] + (double)M[0];
+            b1 += tg * gk;
+            b4 += tg * xxgk;
+            b2 += ((double)P[0] - (double)M[0]) * xgk;
+            b3 += ((double)P[1] + (double)M[1]) * gk;
+            b6 += ((double)P[1] - (double)M[1]) * xgk;
+            b5 += ((double)P[2] + (double)M[2]) * gk;
+        }
+        float* d = R + ((size_t)y * w + x) * 5;
+        d[1] = (float)(b2 * pc.ig11);
+        d[0] = (float)(b3 * pc.ig11);
+        d[3] = (float)(b1 * pc.ig03 + b4 * pc.ig33);
+        d[2] = (float)(b1 * pc.ig03 + b5 * pc.ig33);
+        d[4] = (float)(b6 * pc.ig55);
+    }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------- level 0 --------
+// Tile PT_W x PT_H of the full-resolution frame. Gray (of:71) over the tile +
+// (PN+1) halo, the level-0 smoothing (GaussianBlur 3x3, sigma 0 -> taps
+// (0.25, 0.5, 0.25), BORDER_REFLECT_101) over tile + PN halo, then the
+// polynomial expansion. blockIdx.z = frame of the batch.
+template <int PN>
+__global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* __restrict__ gray_out,
+                                                   const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
+                                                   long long a0)
+{
+    constexpr int HG = PN + 1, GW = PT_W + 2 * HG, GH = PT_H + 2 * HG;
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    __shared__ float sg[GH * GW];
+    __shared__ float sI[IH * IW];
+    __shared__ float sv[PT_H * IW * 3];
+    const int tid = threadIdx.x, t = blockIdx.z;
+    const int W = g.W, H = g.H;
+    const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
+    const uint8_t* f = bgr + (size_t)t * fstride;
+    uint8_t* go = gray_out + (size_t)t * W * H;
+    for (int idx = tid; idx < GH * GW; idx += 256) {
+        const int i = idx / GW, j = idx - i * GW;
+        const int y = y0 - HG + i, x = x0 - HG + j;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;
+        const uint8_t* p = f + (size_t)y * pitch + 3 * x;
+        const uint32_t v = gray_px(p[0], p[1], p[2]);
+        sg[idx] = (float)v;
+        if (i >= HG && i < HG + PT_H && j >= HG && j < HG + PT_W) go[(size_t)y * W + x] = (uint8_t)v;
+    }
+    __syncthreads();
+    // I = blur3(gray): horizontal pass at the 3 rows, then vertical (oc_blur_f32)
+    const float kc = lv.kf[1], ks = lv.kf[2];
+    for (int idx = tid; idx < IH * IW; idx += 256) {
+        const int i = idx / IW, j = idx - i * IW;
+        const int y = y0 - PN + i, x = x0 - PN + j;
+        if (y < 0 || y >= H || x < 0 || x >= W) continue;
+        const int xl = reflect101(x - 1, W) - (x0 - HG), xc = x - (x0 - HG), xr = reflect101(x + 1, W) - (x0 - HG);
+        float hv[3];
+        const int ys[3] = {reflect101(y - 1, H), y, reflect101(y + 1, H)};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float* s = sg + (ys[q] - (y0 - HG)) * GW;
+            float acc = kc * s[xc];
+            acc += ks * (s[xl] + s[xr]);
+            hv[q] = acc;
+        }
+        float acc = kc * hv[1];
+        acc += ks * (hv[0] + hv[2]);
+        sI[idx] = acc;
+    }
+    __syncthreads();
+    float* R = lv.R + (size_t)ring(a0 + t, g.RS) * W * H * 5;
+    poly_tile<PN>(sI, sv, g.pc, x0, y0, W, H, R);
+}
+
+// ----------------------------------------------------------- level k > 0 ----
+// Horizontal smoothing pass (oc_blur_f32, first loop) of the full-resolution
+// gray at the 2w source columns the resize reads: tmpc[y][2dx] at xt[dx].s0,
+// tmpc[y][2dx+1] at xt[dx].s1.
+__global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
+{
+    const int j = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, t = blockIdx.z;
+    const int W = g.W, H = g.H;
+    if (j >= 2 * lv.w) return;
+    const LinTap tp = lv.xt[j >> 1];
+    const int c = (j & 1) ? tp.s1 : tp.s0;
+    const uint8_t* s = gray + (size_t)t * W * H + (size_t)y * W;
+    const int r = lv.r;
+    float acc = lv.kf[r] * (float)s[c];
+    for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
+    lv.tmpc[(size_t)t * H * 2 * lv.w + (size_t)y * 2 * lv.w + j] = acc;
+}
+
+// Vertical smoothing pass at the rows the resize reads, the INTER_LINEAR
+// combination (oc_resize_linear_f32) over tile + PN halo, then the polynomial
+// expansion of the level image.
+template <int PN>
+__global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long a0)
+{
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    __shared__ float sI[IH * IW];
+    __shared__ float sv[PT_H * IW * 3];
+    const int tid = threadIdx.x, t = blockIdx.z;
+    const int H = g.H, w = lv.w, h = lv.h, r = lv.r;
+    const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
+    const float* T = lv.tmpc + (size_t)t * H * 2 * w;
+    const size_t TS = 2 * (size_t)w;
+    auto vblur = [&](int row, int col) {   // blurred full-res value at (row, source column slot col)
+        float acc = lv.kf[r] * T[(size_t)row * TS + col];
+        for (int i = 1; i <= r; ++i)
+            acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * TS + col] + T[(size_t)reflect101(row + i, H) * TS + col]);
+        return acc;
+    };
+    for (int idx = tid; idx < IH * IW; idx += 256) {
+        const int i = idx / IW, j = idx - i * IW;
+        const int y = y0 - PN + i, x = x0 - PN + j;
+        if (y < 0 || y >= h || x < 0 || x >= w) continue;
+        const LinTap ty = lv.yt[y], tx = lv.xt[x];
+        const float v00 = vblur(ty.s0, 2 * x), v01 = vblur(ty.s0, 2 * x + 1);
+        const float v10 = vblur(ty.s1, 2 * x), v11 = vblur(ty.s1, 2 * x + 1);
+        const float t0 = v00 * tx.w0 + v01 * tx.w1;
+        const float t1 = v10 * tx.w0 + v11 * tx.w1;
+        sI[idx] = t0 * ty.w0 + t1 * ty.w1;
+    }
+    __syncthreads();
+    float* R = lv.R + (size_t)ring(a0 + t, g.RS) * w * h * 5;
+    poly_tile<PN>(sI, sv, g.pc, x0, y0, w, h, R);
+}
+
+// -------------------------------------------------------------------- flow --
+// One Farneback iteration of level `lv` for every frame of the batch
+// (blockIdx.z). Tile FL_W x FL_H; LDS holds M (5 floats) over the tile + m halo
+// (replicated borders), then — aliased over it — the vertical box sums.
+//   src_mode 0: flow_in = 0 (coarsest level, first iteration)
+//            1: flow_in = INTER_LINEAR upsample of the coarser level's final
+//               flow, times (float)(1/pyr_scale)
+//            2: flow_in = this level's previous iteration
+//   last:    the finest level's last iteration: |flow| > thr bits -> mring
+struct FlowArgs {
+    OfGeom g;
+    Level lv;
+    const float* src;    // flow_in (mode 1: coarser level's, mode 2: this level's), n frames
+    int sw, sh;          // dims of src (mode 1)
+    float* dst;          // flow out, n frames (nullable when last)
+    long long a0;
+    int src_mode, last;
+    uint64_t* mring;
+    float* dbg_flow;     // last && nullable: frame n-1's flow
+    int n;
+};
+
+__global__ void __launch_bounds__(256) k_flow(FlowArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_d[];
+    float* sM = reinterpret_cast<float*>(lds_d);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = blockIdx.z;
+    const OfGeom& g = A.g;
+    const int w = A.lv.w, h = A.lv.h, m = g.m;
+    const int RW = FL_W + 2 * m, RH = FL_H + 2 * m;
+    const int x0 = blockIdx.x * FL_W, y0 = blockIdx.y * FL_H;
+    const size_t lvpx = (size_t)w * h;
+    const long long a = A.a0 + t;
+    const float* __restrict__ R0 = A.lv.R + (size_t)ring(a - 1, g.RS) * lvpx * 5;
+    const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
+    const float* src = A.src ? A.src + (size_t)t * (A.src_mode == 1 ? (size_t)A.sw * A.sh : lvpx) * 2 : nullptr;
+    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
+
+    // ---- FarnebackUpdateMatrices over tile + halo (oc_update_matrices)
+    for (int idx = tid; idx < RH * RW; idx += 256) {
+        const int i = idx / RW, j = idx - i * RW;
+        const int y = y0 - m + i, x = x0 - m + j;
+        if (y < 0 || y >= h || x < 0 || x >= w) continue;
+        float dx = 0.f, dy = 0.f;
+        if (A.src_mode == 2) {
+            dx = src[((size_t)y * w + x) * 2];
+            dy = src[((size_t)y * w + x) * 2 + 1];
+        } else if (A.src_mode == 1) {
+            const LinTap ty = A.lv.uy[y], tx = A.lv.ux[x];
+            const float* r0 = src + (size_t)ty.s0 * A.sw * 2;
+            const float* r1 = src + (size_t)ty.s1 * A.sw * 2;
+            float v[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float t0 = r0[tx.s0 * 2 + c] * tx.w0 + r0[tx.s1 * 2 + c] * tx.w1;
+                const float t1 = r1[tx.s0 * 2 + c] * tx.w0 + r1[tx.s1 * 2 + c] * tx.w1;
+                v[c] = t0 * ty.w0 + t1 * ty.w1;
+            }
+            dx = v[0] * g.up;
+            dy = v[1] * g.up;
+        }
+        const float* r0 = R0 + ((size_t)y * w + x) * 5;
+        float fx = (float)x + dx, fy = (float)y + dy;
+        const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
+        float r2, r3, r4, r5, r6;
+        fx -= (float)x1;
+        fy -= (float)y1;
+        if ((unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1)) {
+            const float* p = R1 + ((size_t)y1 * w + x1) * 5;
+            const float* q = p + (size_t)w * 5;
+            const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+            r2 = a00 * p[0] + a01 * p[5] + a10 * q[0] + a11 * q[5];
+            r3 = a00 * p[1] + a01 * p[6] + a10 * q[1] + a11 * q[6];
+            r4 = a00 * p[2] + a01 * p[7] + a10 * q[2] + a11 * q[7];
+            r5 = a00 * p[3] + a01 * p[8] + a10 * q[3] + a11 * q[8];
+            r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
+            r4 = (r0[2] + r4) * 0.5f;
+            r5 = (r0[3] + r5) * 0.5f;
+            r6 = (r0[4] + r6) * 0.25f;
+        } else {
+            r2 = r3 = 0.f;
+            r4 = r0[2];
+            r5 = r0[3];
+            r6 = r0[4] * 0.5f;
+        }
+        r2 = (r0[0] - r2) * 0.5f;
+        r3 = (r0[1] - r3) * 0.5f;
+        r2 += r4 * dy + r6 * dx;
+        r3 += r6 * dy + r5 * dx;
+        if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
+            const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
+                                (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+            r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+        }
+        float* M = sM + (size_t)idx * 5;
+        M[0] = r4 * r4 + r6 * r6;
+        M[1] = (r4 + r5) * r6;
+        M[2] = r5 * r5 + r6 * r6;
+        M[3] = r4 * r2 + r6 * r3;
+        M[4] = r6 * r2 + r5 * r3;
+    }
+    __syncthreads();
+
+    // ---- vertical box sums (double, rows in order), into registers, then
+    // aliased over sM: FL_H x RW x 5 doubles
+    constexpr int VMAX = (FL_H * (FL_W + 2 * OF_MAX_BOX_M) + 255) / 256;
+    double vs[VMAX][5];
+    const int nv = FL_H * RW;
+#pragma unroll
+    for (int q = 0; q < VMAX; ++q) {
+        const int idx = tid + 256 * q;
+        if (idx >= nv) break;
+        const int i = idx / RW, j = idx - i * RW;
+        const int y = y0 + i, x = x0 - m + j;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) vs[q][c] = 0.0;
+        if (y >= h || x < 0 || x >= w) continue;
+        double s[5] = {0, 0, 0, 0, 0};
+        for (int jj = -m; jj <= m; ++jj) {
+            const float* M = sM + (size_t)((min(max(y + jj, 0), h - 1) - (y0 - m)) * RW + j) * 5;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) s[c] += (double)M[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 5; ++c) vs[q][c] = s[c];
+    }
+    __syncthreads();
+    double* sV = lds_d;
+#pragma unroll
+    for (int q = 0; q < VMAX; ++q) {
+        const int idx = tid + 256 * q;
+        if (idx >= nv) break;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) sV[(size_t)idx * 5 + c] = vs[q][c];
+    }
+    __syncthreads();
+
+    // ---- horizontal box sums, flow = G^-1 h (oc_update_flow_box); one wave per row
+    float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
+    unsigned long long nmot = 0;
+    for (int i = wave; i < FL_H; i += 4) {
+        const int y = y0 + i, x = x0 + lane;
+        const bool act = y < h && x < w;
+        float fxo = 0.f, fyo = 0.f;
+        if (act) {
+            double hs[5] = {0, 0, 0, 0, 0};
+            for (int ii = -m; ii <= m; ++ii) {
+                const double* v = sV + (size_t)(i * RW + (min(max(x + ii, 0), w - 1) - (x0 - m))) * 5;
+#pragma unroll
+                for (int c = 0; c < 5; ++c) hs[c] += v[c];
+            }
+            const double g11 = hs[0] * g.box_scale, g12 = hs[1] * g.box_scale, g22 = hs[2] * g.box_scale;
+            const double h1 = hs[3] * g.box_scale, h2 = hs[4] * g.box_scale;
+            const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+            fxo = (float)((g11 * h2 - g12 * h1) * idet);
+            fyo = (float)((g22 * h1 - g12 * h2) * idet);
+        }
+        if (!A.last) {
+            if (act) {
+                dst[((size_t)y * w + x) * 2] = fxo;
+                dst[((size_t)y * w + x) * 2 + 1] = fyo;
+            }
+        } else {
+            // of:82-83: cartToPolar magnitude (float) > flow_threshold
+            const float mag = sqrtf(fxo * fxo + fyo * fyo);
+            const bool bit = act && mag > g.flow_thr;
+            const unsigned long long word = __ballot(bit);
+            if (lane == 0 && y < h)
+                A.mring[(size_t)ring(a, g.RB) * h * g.WW + (size_t)y * g.WW + (x0 >> 6)] = word;
+            nmot += (unsigned long long)__popcll(word);
+            if (A.dbg_flow && t == A.n - 1 && act) {
+                A.dbg_flow[((size_t)y * w + x) * 2] = fxo;
+                A.dbg_flow[((size_t)y * w + x) * 2 + 1] = fyo;
+            }
+        }
+    }
+    (void)nmot;
+}
+
+// -------------------------------------------------------------------- vote --
+// of:84-86: count of the last L = min(frames, window) raw masks (the deque),
+// smoothed = count >= vthr[L]. One lane per 16 px (a u16 of a mask word), the
+// counts of its 16 px as bytes in 4 registers, frames walked in order.
+__global__ void __launch_bounds__(256) k_vote(OfGeom g, OfBufs b, long long a0, int window, int n)
+{
+    const int H = g.H, WW = g.WW;
+    const size_t nchunk = (size_t)H * WW * 4;
+    const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const bool act = c < nchunk;
+    const size_t cc = act ? c : 0;
+    uint32_t cnt[4];
+    const uint4 c4 = reinterpret_cast<const uint4*>(b.cnt)[cc];
+    cnt[0] = c4.x; cnt[1] = c4.y; cnt[2] = c4.z; cnt[3] = c4.w;
+    const uint16_t* mr = reinterpret_cast<const uint16_t*>(b.mring);
+    uint16_t* sb = reinterpret_cast<uint16_t*>(b.sbits);
+    const size_t plane16 = (size_t)H * WW * 4;
+    unsigned long long nmot = 0;
+    auto spread = [](uint32_t nib) {   // 4 bits -> 4 bytes of 0/1
+        return (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+    };
+    for (int t = 0; t < n; ++t) {
+        const long long a = a0 + t;
+        const uint32_t nw = mr[(size_t)ring(a, g.RB) * plane16 + cc];
+        const uint32_t ow = a - window >= 1 ? mr[(size_t)ring(a - window, g.RB) * plane16 + cc] : 0u;
+        const int L = (int)min<long long>(a, (long long)window);
+        const uint32_t thr = b.vthr[L];
+        const uint32_t bias = (0x80u - thr) * 0x01010101u;
+        uint32_t out = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cnt[j] = cnt[j] + spread((nw >> (4 * j)) & 15u) - spread((ow >> (4 * j)) & 15u);
+            const uint32_t ge = (cnt[j] + bias) & 0x80808080u;   // count <= 127, thr <= 128: no carries
+            out |= (((ge >> 7) & 1u) | ((ge >> 14) & 2u) | ((ge >> 21) & 4u) | ((ge >> 28) & 8u)) << (4 * j);
+        }
+        nmot += (unsigned long long)__popc(nw);
+        if (act) sb[(size_t)t * plane16 + c] = (uint16_t)out;
+    }
+    if (act) reinterpret_cast<uint4*>(b.cnt)[c] = make_uint4(cnt[0], cnt[1], cnt[2], cnt[3]);
+    if (!act) nmot = 0;
+    for (int d = 32; d >= 1; d >>= 1) nmot += __shfl_xor(nmot, d, 64);
+    if ((threadIdx.x & 63) == 0 && nmot) atomicAdd(b.stats + STAT_SLOT(blockIdx.x) * 4 + 1, nmot);
+}
+
+// ---------------------------------------------------------- morphology + CCL
+// One workgroup per band of BH rows (one wave per row) of frame blockIdx.y.
+// MORPH_CLOSE then MORPH_OPEN with [[0,1],[1,1]] (anchor (1,1)): every pass
+// reads (x, y), (x-1, y), (x, y-1); out-of-image neighbours are ignored
+// (0 for dilate, 1 for erode). Four passes need 4 halo rows above the band.
+// Then the run index of each row, union-find of the band's runs (8-connected)
+// in LDS, band-local roots published as global ids (id = y*CAP + k), and
+// every run's bounding box initialised to itself.
+// Dynamic LDS: 2 x (BH+4) x WW u64 morph rows | run index (2 BH WW u64 +
+// 2 BH (WW+1) u16) | BH*CAP u32 parents.
+__global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int WW = g.WW, W = g.W, H = g.H, CAP = g.CAP;
+    const int t = blockIdx.y;
+    const size_t plane = (size_t)H * WW, nr = (size_t)H * CAP;
+    const uint64_t* sb = B.sbits + (size_t)t * plane;
+    uint64_t* ob = B.obits + (size_t)t * plane;
+    const int NRW = BH + 4;
+    uint64_t* mA = lds;
+    uint64_t* mB = mA + NRW * WW;
+    uint64_t* l_st = mB + NRW * WW;
+    uint64_t* l_en = l_st + BH * WW;
+    uint16_t* l_ps = reinterpret_cast<uint16_t*>(l_en + BH * WW);
+    uint16_t* l_pe = l_ps + BH * (WW + 1);
+    uint32_t* lp = reinterpret_cast<uint32_t*>(l_pe + BH * (WW + 1));
+    const int tid = threadIdx.x, nth = blockDim.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int y0 = blockIdx.x * BH;
+    const uint64_t lastmask = (W & 63) ? ((1ull << (W & 63)) - 1) : ~0ull;
+
+    for (int idx = tid; idx < NRW * WW; idx += nth) {
+        const int r = idx / WW, wi = idx - r * WW, y = y0 - 4 + r;
+        mA[idx] = (y >= 0 && y < H) ? sb[(size_t)y * WW + wi] : 0ull;
+    }
+    __syncthreads();
+    // passes: dilate A->B, erode B->A, erode A->B, dilate B->A
+#pragma unroll
+    for (int p = 1; p <= 4; ++p) {
+        const uint64_t* src = (p & 1) ? mA : mB;
+        uint64_t* dst = (p & 1) ? mB : mA;
+        const bool dil = p == 1 || p == 4;
+        for (int idx = p * WW + tid; idx < NRW * WW; idx += nth) {
+            const int r = idx / WW, wi = idx - r * WW, y = y0 - 4 + r;
+            if (y < 0 || y >= H) continue;
+            const uint64_t v = src[idx];
+            const uint64_t lb = wi > 0 ? (src[idx - 1] >> 63) : (dil ? 0ull : 1ull);
+            const uint64_t left = (v << 1) | lb;
+            const uint64_t up = y > 0 ? src[idx - WW] : (dil ? 0ull : ~0ull);
+            uint64_t o = dil ? (v | left | up) : (v & left & up);
+            if (wi == WW - 1) o &= lastmask;
+            dst[idx] = o;
+        }
+        __syncthreads();
+    }
+    // morphed rows of the band -> global
+    for (int idx = tid; idx < BH * WW; idx += nth) {
+        const int r = idx / WW, wi = idx - r * WW, y = y0 + r;
+        if (y < H) ob[(size_t)y * WW + wi] = mA[(r + 4) * WW + wi];
+    }
+
+    // run index + local union-find (fg, 8-connected)
+    const int y = y0 + wave;
+    const bool act = wave < BH && y < H;
+    uint16_t* rs = B.rs + (size_t)t * nr;
+    uint16_t* re = B.re + (size_t)t * nr;
+    uint32_t* fpar = B.fpar + (size_t)t * nr;
+    uint32_t* bx0 = B.bx0 + (size_t)t * nr;
+    uint32_t* bx1 = B.bx1 + (size_t)t * nr;
+    uint32_t* by0 = B.by0 + (size_t)t * nr;
+    uint32_t* by1 = B.by1 + (size_t)t * nr;
+    const uint32_t base = (uint32_t)y * CAP;
+    uint64_t* st = l_st + wave * WW;
+    uint64_t* en = l_en + wave * WW;
+    uint16_t* ps = l_ps + wave * (WW + 1);
+    uint16_t* pe = l_pe + wave * (WW + 1);
+    int n = 0;
+    if (act) {
+        n = build_row_idx(mA + (wave + 4) * WW, WW, W, st, en, ps, pe, nullptr);
+        for (int i = lane; i < WW; i += 64) {
+            uint64_t s = st[i], e = en[i];
+            int ks = ps[i], ke = pe[i];
+            while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
+            while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
+        }
+        for (int k = lane; k < n; k += 64) lp[wave * CAP + k] = wave * CAP + k;
+        if (lane == 0) B.nfg[(size_t)t * H + y] = (uint32_t)n;
+    }
+    __syncthreads();
+    if (act && wave + 1 < BH && y + 1 < H) {
+        const uint32_t f0 = wave * CAP, f1 = f0 + CAP;
+        const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
+        for (int i = lane; i < n; i += 64) {
+            const int a = select_k(r0.st, r0.ps, WW, i), b = select_k(r0.en, r0.pe, WW, i);
+            const int j0 = rank_le(r1.en, r1.pe, WW, a - 2), j1 = rank_le(r1.st, r1.ps, WW, b + 1);
+            for (int j = j0; j < j1; ++j) lunion(lp, f0 + i, f1 + j);
+        }
+    }
+    __syncthreads();
+    if (act) {
+        for (int k = lane; k < n; k += 64) {
+            const uint32_t r = lfind(lp, wave * CAP + k);
+            fpar[base + k] = (uint32_t)(y0 + r / CAP) * CAP + r % CAP;
+            const uint32_t s = rs[base + k], e = re[base + k];
+            bx0[base + k] = s;
+            bx1[base + k] = e;
+            by0[base + k] = (uint32_t)y;
+            by1[base + k] = (uint32_t)y;
+        }
+    }
+}
+
+// One wave per band seam (rows b*BH-1, b*BH) of frame blockIdx.y: global
+// unions of the runs that touch (8-connected) across it.
+__global__ void __launch_bounds__(64) k_of_merge(OfGeom g, OfBufs B, int BH)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const int WW = g.WW, t = blockIdx.y;
+    const int y = (blockIdx.x + 1) * BH - 1;
+    if (y + 1 >= g.H) return;
+    const size_t plane = (size_t)g.H * WW, nr = (size_t)g.H * g.CAP;
+    const uint64_t* ob = B.obits + (size_t)t * plane;
+    uint32_t* fpar = B.fpar + (size_t)t * nr;
+    uint64_t* st = lds;
+    uint64_t* en = st + 2 * WW;
+    uint16_t* ps = reinterpret_cast<uint16_t*>(en + 2 * WW);
+    uint16_t* pe = ps + 2 * (WW + 1);
+    const int n0 = build_row_idx(ob + (size_t)y * WW, WW, g.W, st, en, ps, pe, nullptr);
+    build_row_idx(ob + (size_t)(y + 1) * WW, WW, g.W, st + WW, en + WW, ps + WW + 1, pe + WW + 1, nullptr);
+    __syncthreads();
+    const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < n0; i += 64) {
+        const int a = select_k(st, ps, WW, i), b = select_k(en, pe, WW, i);
+        const int j0 = rank_le(en + WW, pe + WW + 1, WW, a - 2), j1 = rank_le(st + WW, ps + WW + 1, WW, b + 1);
+        for (int j = j0; j < j1; ++j) uf_union(fpar, b0 + i, b1 + j);
+    }
+}
+
+// One wave per row: every run's root (path-compressed), its extents folded
+// into the root's bounding box; roots appended to the frame's root list.
+__global__ void __launch_bounds__(64) k_of_bbox(OfGeom g, OfBufs B)
+{
+    const int y = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
+    const size_t nr = (size_t)g.H * g.CAP;
+    uint32_t* fpar = B.fpar + (size_t)t * nr;
+    const uint16_t* rs = B.rs + (size_t)t * nr;
+    const uint16_t* re = B.re + (size_t)t * nr;
+    const int n = (int)B.nfg[(size_t)t * g.H + y];
+    const uint32_t base = (uint32_t)y * g.CAP;
+    int comps = 0;
+    for (int k = lane; k < n; k += 64) {
+        const uint32_t id = base + k;
+        const uint32_t r = uf_find(fpar, id);
+        atomicMin(fpar + id, r);
+        if (r == id) {
+            const uint32_t pos = atomicAdd(B.nroots + t, 1u);
+            B.roots[(size_t)t * nr + pos] = id;
+            ++comps;
+        } else {
+            atomicMin(B.bx0 + (size_t)t * nr + r, (uint32_t)rs[id]);
+            atomicMax(B.bx1 + (size_t)t * nr + r, (uint32_t)re[id]);
+            atomicMin(B.by0 + (size_t)t * nr + r, (uint32_t)y);
+            atomicMax(B.by1 + (size_t)t * nr + r, (uint32_t)y);
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) comps += __shfl_xor(comps, d, 64);
+    if (lane == 0 && comps) atomicAdd(B.stats + STAT_SLOT(y) * 4 + 2, (unsigned long long)comps);
+}
+
+// of:93-97: cv2.rectangle(mask, (x, y), (x+w, y+h), 255, -1) of every
+// component's bounding rectangle, i.e. rows y0..y1+1 x cols x0..x1+1 (clipped),
+// OR-painted as bits. One wave per root (grid-stride), lanes over (row, word).
+__global__ void __launch_bounds__(256) k_of_rect(OfGeom g, OfBufs B)
+{
+    const int t = blockIdx.y, lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), nwv = gridDim.x * 4;
+    const size_t nr = (size_t)g.H * g.CAP;
+    const uint32_t cnt = B.nroots[t];
+    uint64_t* rb = B.rbits + (size_t)t * g.H * g.WW;
+    for (uint32_t i = wv; i < cnt; i += nwv) {
+        const uint32_t r = B.roots[(size_t)t * nr + i];
+        const int xa = (int)B.bx0[(size_t)t * nr + r], xb = min((int)B.bx1[(size_t)t * nr + r] + 1, g.W - 1);
+        const int ya = (int)B.by0[(size_t)t * nr + r], yb = min((int)B.by1[(size_t)t * nr + r] + 1, g.H - 1);
+        const int ws = xa >> 6, we = xb >> 6, nw = we - ws + 1;
+        const int tot = (yb - ya + 1) * nw;
+        for (int q = lane; q < tot; q += 64) {
+            const int row = ya + q / nw, wi = ws + q % nw;
+            uint64_t mk = ~0ull;
+            if (wi == ws) mk &= ~0ull << (xa & 63);
+            if (wi == we) mk &= ~0ull >> (63 - (xb & 63));
+            atomicOr(reinterpret_cast<unsigned long long*>(rb + (size_t)row * g.WW + wi), (unsigned long long)mk);
+        }
+    }
+}
+
+// ----------------------------------------------------------------- output ---
+// One lane per 8x8 block (64 blocks across, one wave per block row, 4 block
+// rows per workgroup), blockIdx.z = frame. compress_with_motion (of:151-183):
+// BGR->YCrCb (of:152); a full block whose mask is all zero (of:159,161) gets
+// each of Y, Cr, Cb DCT-quantised (of:162-168); all pixels YCrCb->BGR
+// (of:170-171); static blocks then BGR->gray->BGR (of:174-183).
+__global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = blockIdx.z;
+    const int W = g.W, H = g.H, WW = g.WW;
+    const int bx = (blockIdx.x * 64 + lane) * 8, by = (blockIdx.y * 4 + wave) * 8;
+    if (bx >= W || by >= H) return;
+    const uint8_t* f = o.bgr + (size_t)t * o.fstride;
+    const uint64_t* rb = B.rbits + (size_t)t * H * WW;
+    uint32_t mrow[8];
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        mrow[i] = (uint32_t)(rb[(size_t)(by + i) * WW + (bx >> 6)] >> (bx & 63)) & 0xffu;
+        any |= mrow[i];
+    }
+    if (o.mask) {
+        uint8_t* mk = o.mask + (size_t)t * o.mstride;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                lo |= ((mrow[i] >> j) & 1u) ? (255u << (8 * j)) : 0u;
+                hi |= ((mrow[i] >> (j + 4)) & 1u) ? (255u << (8 * j)) : 0u;
+            }
+            *reinterpret_cast<uint2*>(mk + (size_t)(by + i) * W + bx) = make_uint2(lo, hi);
+        }
+    }
+    if (!o.compressed) return;
+    const bool is_static = any == 0;
+    // YCrCb planes of the block, 8 px per row as two u32 per channel
+    uint32_t yc[3][8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * o.pitch + 3 * bx);
+        uint32_t px[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) px[d] = src[d];
+        uint32_t Y[2] = {0, 0}, Cr[2] = {0, 0}, Cb[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int b = (px[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
+            const int gg = (px[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
+            const int r = (px[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+            const int yv = descale14(b * 1868 + gg * 9617 + r * 4899);
+            const uint32_t cr = satu8(descale14((r - yv) * 11682 + (128 << 14)));
+            const uint32_t cb = satu8(descale14((b - yv) * 9241 + (128 << 14)));
+            Y[j >> 2] |= (uint32_t)yv << (8 * (j & 3));
+            Cr[j >> 2] |= cr << (8 * (j & 3));
+            Cb[j >> 2] |= cb << (8 * (j & 3));
+        }
+        yc[0][i][0] = Y[0]; yc[0][i][1] = Y[1];
+        yc[1][i][0] = Cr[0]; yc[1][i][1] = Cr[1];
+        yc[2][i][0] = Cb[0]; yc[2][i][1] = Cb[1];
+    }
+    const bool full = bx + 8 <= W && by + 8 <= H;
+    if (is_static && full) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float X[64];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) X[i * 8 + j] = (float)((yc[c][i][j >> 2] >> (8 * (j & 3))) & 255) - 128.0f;
+            block_dct_quant<8>(X, o.M, o.quant);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t v2[2] = {0, 0};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float v = X[i * 8 + j] + 128.0f;
+                    v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+                    v2[j >> 2] |= ((uint32_t)v & 255u) << (8 * (j & 3));
+                }
+                yc[c][i][0] = v2[0];
+                yc[c][i][1] = v2[1];
+            }
+        }
+    }
+    uint8_t* cpf = o.compressed + (size_t)t * o.ostride;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint8_t ob[24];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int yv = (yc[0][i][j >> 2] >> (8 * (j & 3))) & 255;
+            const int cr = (int)((yc[1][i][j >> 2] >> (8 * (j & 3))) & 255) - 128;
+            const int cb = (int)((yc[2][i][j >> 2] >> (8 * (j & 3))) & 255) - 128;
+            uint32_t b = satu8(yv + descale14(cb * 29049));
+            uint32_t gg = satu8(yv + descale14(cb * -5636 + cr * -11698));
+            uint32_t r = satu8(yv + descale14(cr * 22987));
+            if (is_static && full) b = gg = r = gray_px(b, gg, r);
+            ob[3 * j] = (uint8_t)b;
+            ob[3 * j + 1] = (uint8_t)gg;
+            ob[3 * j + 2] = (uint8_t)r;
+        }
+        uint32_t* d = reinterpret_cast<uint32_t*>(cpf + (size_t)(by + i) * 3 * W + 3 * bx);
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+            d[q] = ob[4 * q] | (ob[4 * q + 1] << 8) | (ob[4 * q + 2] << 16) | ((uint32_t)ob[4 * q + 3] << 24);
+    }
+}
+
+// Static-block counter (separate tiny pass keeps k_of_out's exits simple).
+__global__ void __launch_bounds__(256) k_of_count_static(OfGeom g, OfBufs B, int n)
+{
+    const int W = g.W, H = g.H, WW = g.WW;
+    const int nbx = W / 8, nby = H / 8;
+    const size_t tot = (size_t)nbx * nby * n;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    bool st = false;
+    if (i < tot) {
+        const int t = (int)(i / ((size_t)nbx * nby));
+        const int rem = (int)(i % ((size_t)nbx * nby));
+        const int byi = rem / nbx, bxi = rem % nbx;
+        const uint64_t* rb = B.rbits + (size_t)t * H * WW;
+        uint32_t any = 0;
+        for (int r = 0; r < 8; ++r) any |= (uint32_t)(rb[(size_t)(byi * 8 + r) * WW + (bxi * 8 >> 6)] >> ((bxi * 8) & 63)) & 0xffu;
+        st = any == 0;
+    }
+    const unsigned long long bal = __ballot(st);
+    if ((threadIdx.x & 63) == 0 && bal)
+        atomicAdd(B.stats + STAT_SLOT(blockIdx.x) * 4 + 3, (unsigned long long)__popcll(bal));
+}
+
+// --------------------------------------------------------------- launchers --
+static int of_band_rows(const OfGeom& g, size_t* lds)
+{
+    int bh = 8;
+    for (;;) {
+        const size_t b = (size_t)16 * (bh + 4) * g.WW + (size_t)16 * bh * g.WW + (size_t)4 * bh * (g.WW + 1) +
+                         (size_t)4 * bh * g.CAP + 16;
+        if (b <= 150 * 1024 || bh == 1) {
+            *lds = b;
+            return bh;
+        }
+        bh >>= 1;
+    }
+}
+
+hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
+                             size_t fstride, long long a0, int n, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    {
+        dim3 grid((g.W + PT_W - 1) / PT_W, (g.H + PT_H - 1) / PT_H, n);
+        if (g.pc.n == 5) hipLaunchKernelGGL(k_of_front0<5>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
+        else hipLaunchKernelGGL(k_of_front0<7>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
+    }
+    for (int k = 1; k <= g.L; ++k) {
+        dim3 gh((2 * lv[k].w + 255) / 256, g.H, n);
+        hipLaunchKernelGGL(k_pyr_h, gh, dim3(256), 0, s, g, lv[k], b.gray);
+        dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);
+        if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, s, g, lv[k], a0);
+        else hipLaunchKernelGGL(k_pyr_poly<7>, gp, dim3(256), 0, s, g, lv[k], a0);
+    }
+    return hipGetLastError();
+}
+
+hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
+                          hipStream_t s)
+{
+    const size_t lds = std::max((size_t)(FL_H + 2 * g.m) * (FL_W + 2 * g.m) * 5 * 4,
+                                (size_t)FL_H * (FL_W + 2 * g.m) * 5 * 8);
+    for (int k = k_hi; k >= k_lo; --k) {
+        const Level& L = lv[k];
+        dim3 grid((L.w + FL_W - 1) / FL_W, (L.h + FL_H - 1) / FL_H, n);
+        for (int it = 0; it < g.iters; ++it) {
+            FlowArgs A{};
+            A.g = g;
+            A.lv = L;
+            A.a0 = a0;
+            A.n = n;
+            if (it > 0) {
+                A.src_mode = 2;
+                A.src = L.flow[(it - 1) & 1];
+            } else if (k < g.L) {
+                A.src_mode = 1;
+                A.src = lv[k + 1].flow[(g.iters - 1) & 1];
+                A.sw = lv[k + 1].w;
+                A.sh = lv[k + 1].h;
+            } else {
+                A.src_mode = 0;
+                A.src = nullptr;
+            }
+            A.last = (k == 0 && it == g.iters - 1);
+            A.dst = A.last ? nullptr : L.flow[it & 1];
+            A.mring = b.mring;
+            A.dbg_flow = b.dbg_flow;
+            hipLaunchKernelGGL(k_flow, grid, dim3(256), lds, s, A);
+        }
+    }
+    return hipGetLastError();
+}
+
+hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s)
+{
+    const size_t nchunk = (size_t)g.H * g.WW * 4;
+    hipLaunchKernelGGL(k_vote, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s, g, b, a0, window, n);
+    size_t lds = 0;
+    const int BH = of_band_rows(g, &lds);
+    const int nb = (g.H + BH - 1) / BH;
+    hipError_t e = hipMemsetAsync(b.nroots, 0, 4 * (size_t)n, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_of_band, dim3(nb, n), dim3(64 * std::max(BH, 4)), lds, s, g, b, BH);
+    if (nb > 1) hipLaunchKernelGGL(k_of_merge, dim3(nb - 1, n), dim3(64), 32 * g.WW + 8 * (g.WW + 1), s, g, b, BH);
+    hipLaunchKernelGGL(k_of_bbox, dim3(g.H, n), dim3(64), 0, s, g, b);
+    if ((e = hipMemsetAsync(b.rbits, 0, 8 * (size_t)g.H * g.WW * n, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_of_rect, dim3(64, n), dim3(256), 0, s, g, b);
+    const size_t nblk = (size_t)(g.W / 8) * (g.H / 8) * n;
+    if (nblk) hipLaunchKernelGGL(k_of_count_static, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, g, b, n);
+    return hipGetLastError();
+}
+
+hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s)
+{
+    if (!o.mask && !o.compressed) return hipSuccess;
+    dim3 grid((g.W / 8 + 63) / 64, (g.H / 8 + 3) / 4, n);
+    hipLaunchKernelGGL(k_of_out, grid, dim3(256), 0, s, g, b, o);
+    return hipGetLastError();
+}
+
+}  // namespace dvc

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 2
+#define DVC_ABI_VERSION 3
 #define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
@@ -208,11 +208,83 @@ typedef struct dvc_of_params {
     int32_t iterations;
     int32_t poly_n;
     double poly_sigma;
-    uint32_t flags;      /* DVC_FLAG_DEVICE_PTRS */
-    uint32_t reserved;
+    uint32_t flags;      /* DVC_FLAG_DEVICE_PTRS | DVC_FLAG_KTIMING | DVC_FLAG_KEEP_PLANES */
+    uint32_t max_batch;  /* 0/1..DVC_MAX_BATCH frames per device launch (see dvc_of_step_batch) */
 } dvc_of_params;
 
 typedef struct dvc_of dvc_of;
+
+/* Cumulative per-handle counters (all frames stepped since prime). */
+typedef struct dvc_of_stats {
+    uint64_t frames;        /* frames stepped                                   */
+    uint64_t motion_px;     /* pixels with |flow| > flow_threshold (of:82-83)   */
+    uint64_t components;    /* 8-connected components of the smoothed mask
+                               after close/open (one rectangle each, of:93-97)  */
+    uint64_t static_blocks; /* full 8x8 blocks with an all-zero mask (of:161)   */
+} dvc_of_stats;
+
+/* Create an OF feed handle on `device` (GPU constraints: width and height
+ * multiples of 8, morph_kernel 2, poly_n 5 or 7, winsize <= 17, window <= 127,
+ * pyramid smoothing kernels <= 63 taps). Replaces the per-video setup at
+ * of:38-62. All launches go to `hip_stream` (NULL: a stream owned by the
+ * handle). */
+int dvc_of_create(const dvc_of_params* params, int device, void* hip_stream, dvc_of** out);
+
+/* Frame 0: gray (of:60) and its pyramid; the vote window is emptied (of:61). */
+int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch);
+
+/* One frame of the fused worker: gray, calcOpticalFlowFarneback(prev, gray),
+ * |flow| > thr, windowed vote, close/open, rectangle mask (of:70-97), and the
+ * motion-gated compression of the same frame with that mask (of:151-183).
+ *   mask        nullable, H*W bytes {0,255}: the frame written to mask.mp4 (of:99)
+ *   compressed  nullable, packed BGR rows of 3*W: the frame written to
+ *               compressed.mp4 (of:185)
+ * Synchronisation as dvc_fd_step. */
+int dvc_of_step(dvc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_t* compressed);
+
+/* n consecutive frames (frame t at bgr + t*frame_stride): the pyramid, every
+ * Farneback iteration, the morphology and the compression run as grids over
+ * tiles x frames; only the vote walks the frames in order. Results identical
+ * to n dvc_of_step calls. Mask t at mask + t*mask_stride, compressed frame t at
+ * compressed + t*out_stride. */
+int dvc_of_step_batch(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, int n,
+                      uint8_t* mask, size_t mask_stride, uint8_t* compressed, size_t out_stride);
+
+int dvc_of_sync(dvc_of* h);
+int dvc_of_get_stats(dvc_of* h, dvc_of_stats* out);
+
+/* Planes of the LAST stepped frame, H*W bytes {0,255} (4: gray 0..255):
+ * 0 |flow| > thr (of:83), 1 vote-smoothed (of:86), 2 after close/open
+ * (of:89-90), 3 rectangle mask (of:93-97), 4 gray (of:71). */
+#define DVC_OF_PLANE_RAW    0
+#define DVC_OF_PLANE_SMOOTH 1
+#define DVC_OF_PLANE_MORPH  2
+#define DVC_OF_PLANE_RECT   3
+#define DVC_OF_PLANE_GRAY   4
+int dvc_of_read_plane(dvc_of* h, int plane, uint8_t* host_dst);
+
+/* The Farneback flow of the last stepped frame, H*W*2 floats (dx, dy), to host
+ * memory (of:72-81). Needs DVC_FLAG_KEEP_PLANES. */
+int dvc_of_read_flow(dvc_of* h, float* host_dst);
+
+/* With DVC_FLAG_KTIMING: total ms and launch count of the finest-level
+ * Farneback iterations (k_flow at level 0, the dominant kernel). */
+int dvc_of_ktime(dvc_of* h, double* total_ms, uint64_t* launches, int reset);
+
+void dvc_of_destroy(dvc_of* h);
+
+/* Parity/debug readback of Farneback intermediates of the LAST stepped frame at
+ * pyramid level `level` (host memory): what 0 = its polynomial expansion R
+ * (h_k*w_k*5 floats), 1 = the previous frame's R, 2 = the flow after the first
+ * iteration (h_k*w_k*2 floats; needs iterations >= 2 or level > 0). *w, *h
+ * (nullable) receive the level size; dst may be NULL to query it. */
+int dvc_of_debug_read(dvc_of* h, int what, int level, void* host_dst, int* w, int* hgt);
+
+/* compress_with_motion for one frame with an arbitrary mask (of:141-185, e.g.
+ * a decoded mask.mp4 frame): host pointers, synchronous. mask: H*W bytes,
+ * nonzero = motion. W, H multiples of 8. */
+int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int width, int height, float quant,
+                    int device, uint8_t* out);
 
 /* The Q8 fixed-point Gaussian taps OpenCV's bit-exact 8U GaussianBlur uses
  * (getGaussianKernelBitExact + error-diffusion rounding to 8 fraction bits).

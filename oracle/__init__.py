@@ -337,7 +337,7 @@ class OfParams(ctypes.Structure):
         ("poly_n", ctypes.c_int32),
         ("poly_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
     ]
 
 
@@ -371,6 +371,10 @@ def _of_lib():
         L.oc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, u8p]
         L.oc_vote_threshold.argtypes = [ctypes.c_double, ctypes.c_int]
         L.oc_fb_levels.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int]
+        L.oc_fb_level_poly.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_double, fp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.oc_update_matrices.argtypes = [fp, fp, fp, ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int]
+        L.oc_update_flow_box.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
         L._of_ready = True
     return L
 
@@ -383,6 +387,32 @@ def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.3, levels=2, winsiz
     _of_lib().oc_farneback(_u8(prev), _u8(nxt), W, H, pyr_scale, levels, winsize, iterations, poly_n, poly_sigma,
                            flow.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
     return flow
+
+
+def _fp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def fb_level_poly(gray: np.ndarray, k: int, pyr_scale=0.3, poly_n=5, poly_sigma=1.1) -> np.ndarray:
+    """Smoothed, resized, polynomial-expanded level k of a gray image (h, w, 5)."""
+    gray = np.ascontiguousarray(gray, np.uint8)
+    H, W = gray.shape
+    R = np.empty((H, W, 5), np.float32)
+    w, h = ctypes.c_int(), ctypes.c_int()
+    _of_lib().oc_fb_level_poly(_u8(gray), W, H, pyr_scale, k, poly_n, poly_sigma, _fp(R), ctypes.byref(w),
+                               ctypes.byref(h))
+    return R.reshape(-1)[: h.value * w.value * 5].reshape(h.value, w.value, 5).copy()
+
+
+def fb_iteration(R0: np.ndarray, R1: np.ndarray, flow: np.ndarray, winsize=9) -> np.ndarray:
+    """One FarnebackUpdateMatrices + FarnebackUpdateFlow_Blur step (flow_in -> flow_out)."""
+    h, w = R0.shape[:2]
+    R0, R1 = np.ascontiguousarray(R0, np.float32), np.ascontiguousarray(R1, np.float32)
+    f = np.ascontiguousarray(flow, np.float32).copy()
+    M = np.empty((h, w, 5), np.float32)
+    _of_lib().oc_update_matrices(_fp(R0), _fp(R1), _fp(f), w, h, _fp(M), 0, h)
+    _of_lib().oc_update_flow_box(_fp(M), w, h, winsize, _fp(f))
+    return f
 
 
 def morph_close_open(m: np.ndarray) -> np.ndarray:

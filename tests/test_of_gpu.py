@@ -1,0 +1,168 @@
+"""GPU parity: the HIP optical-flow path vs the CPU oracle, through the C-ABI.
+
+Every float and double expression of the Farneback restatement runs in the
+same order on both sides (-ffp-contract=off), so the bar is bit-exact for the
+flow itself (float32 per component), every mask plane (raw |flow| > thr, vote,
+close/open, rectangles) and every compressed frame.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PLANES = {"raw": 0, "smooth": 1, "morph": 2, "rect": 3}
+
+
+def _first_diff(g, r):
+    d = np.argwhere(g != r)
+    return f"{len(d)} differ, first {d[:4].tolist()}"
+
+
+def _run_pair(dvc_amd, oracle, frames, batch=0, **kw):
+    """Per-frame (batch=0) or batched GPU run vs the oracle; returns GPU stats."""
+    H, W = frames.shape[1:3]
+    okw = {k: v for k, v in kw.items() if k in ("flow_threshold", "alpha_fraction", "window_size", "morph_kernel")}
+    gpu = dvc_amd.OFWorker(W, H, device=0, keep_planes=True, max_batch=max(batch, 1), **kw)
+    ref = oracle.OracleOF(W, H, **okw)
+    gpu.prime(frames[0])
+    ref.prime(frames[0])
+    motion = comps = static = 0
+    rmasks, rcps = [], []
+    for t in range(1, len(frames)):
+        rmask, rcp, rflow = ref.step(frames[t])
+        rmasks.append(rmask)
+        rcps.append(rcp)
+        raw = ref.plane(0)
+        motion += int((raw > 0).sum())
+        comps += oracle.rect_mask(ref.plane(2))[1]
+        static += int((rmask.reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3)) == 0).sum())
+        if batch:
+            continue
+        mask, cp = gpu.step(frames[t])
+        flow = gpu.flow()
+        if not np.array_equal(flow.view(np.uint32), rflow.view(np.uint32)):
+            err = np.abs(flow - rflow).max()
+            raise AssertionError(f"flow differs at frame {t}: {_first_diff(flow, rflow)}, max abs {err}")
+        for name, idx in PLANES.items():
+            g, r = gpu.plane(idx), ref.plane(idx)
+            assert np.array_equal(g, r), f"{name} plane differs at frame {t}: {_first_diff(g, r)}"
+        assert np.array_equal(mask, rmask), f"mask differs at frame {t}"
+        if not np.array_equal(cp, rcp):
+            diff = np.abs(cp.astype(int) - rcp.astype(int))
+            raise AssertionError(f"compressed differs at frame {t}: {(diff > 0).any(-1).sum()} px, max {diff.max()}")
+    if batch:
+        masks, cps = gpu.step_batch(frames[1:])
+        for t in range(len(frames) - 1):
+            assert np.array_equal(masks[t], rmasks[t]), f"batched mask differs at frame {t + 1}"
+            assert np.array_equal(cps[t], rcps[t]), f"batched compressed differs at frame {t + 1}"
+    st = gpu.stats()
+    assert st == {"frames": len(frames) - 1, "motion_px": motion, "components": comps, "static_blocks": static}, st
+    gpu.close()
+    ref.close()
+    return st
+
+
+@pytest.mark.parametrize("W,H", [(160, 96), (640, 360)])
+def test_of_stages(gpu_lib, oracle_lib, W, H):
+    """Stage by stage on one frame pair: gray, the polynomial expansion of every
+    pyramid level, the coarsest level's first iteration, the final flow."""
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, 2, seed=1)
+    gpu = gpu_lib.OFWorker(W, H, keep_planes=True)
+    gpu.prime(frames[0])
+    gpu.step(frames[1])
+    g0, g1 = oracle_lib.bgr2gray(frames[0]), oracle_lib.bgr2gray(frames[1])
+    assert np.array_equal(gpu.plane(gpu_lib._native.OF_PLANE_GRAY), g1), "gray"
+    L = int(oracle_lib._of_lib().oc_fb_levels(W, H, 0.3, 2))
+    for k in range(L + 1):
+        for what, g in ((1, g0), (0, g1)):
+            got, want = gpu.debug_read(what, k), oracle_lib.fb_level_poly(g, k)
+            assert got.shape == want.shape, (k, got.shape, want.shape)
+            if not np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                raise AssertionError(f"R level {k} ({'prev' if what else 'cur'}): {_first_diff(got, want)}, "
+                                     f"max abs {np.abs(got - want).max()}")
+    R0, R1 = oracle_lib.fb_level_poly(g0, L), oracle_lib.fb_level_poly(g1, L)
+    f1 = oracle_lib.fb_iteration(R0, R1, np.zeros(R0.shape[:2] + (2,), np.float32))
+    got = gpu.debug_read(2, L)
+    assert np.array_equal(got.view(np.uint32), f1.view(np.uint32)), f"iteration 0 flow: {_first_diff(got, f1)}"
+    want = oracle_lib.farneback(g0, g1)
+    got = gpu.flow()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"final flow: {_first_diff(got, want)}"
+    gpu.close()
+
+
+@pytest.mark.parametrize("W,H,n,seed,noisy", [
+    (160, 96, 6, 1, False),      # 1 pyramid level
+    (320, 176, 6, 2, False),     # 2 levels
+    (640, 360, 5, 0, False),     # 3 levels
+    (640, 360, 4, 5, True),
+])
+def test_of_parity_synthetic(gpu_lib, oracle_lib, W, H, n, seed, noisy):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=seed, noisy=noisy))
+
+
+def test_of_parity_1080p(gpu_lib, oracle_lib):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(1920, 1080, 3, seed=3))
+
+
+def test_of_parity_window_eviction(gpu_lib, oracle_lib):
+    """window 3 over 9 frames: the deque drops masks (of:84, maxlen)."""
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(320, 176, 9, seed=4, n_objects=4), window_size=3, alpha_fraction=0.4)
+
+
+def test_of_parity_random_frames(gpu_lib, oracle_lib):
+    rng = np.random.default_rng(11)
+    _run_pair(gpu_lib, oracle_lib, rng.integers(0, 256, (4, 96, 128, 3), dtype=np.uint8), flow_threshold=2.0)
+
+
+@pytest.mark.parametrize("batch", [2, 4])
+def test_of_batched_equals_oracle(gpu_lib, oracle_lib, batch):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(320, 176, 10, seed=6, noisy=True), batch=batch, window_size=4)
+
+
+def test_of_device_pointers(gpu_lib, oracle_lib):
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = clip(320, 176, 5, seed=8)
+    n, H, W = frames.shape[:3]
+    d_in = torch.from_numpy(frames).to("cuda:0")
+    d_mask = torch.empty((n - 1, H, W), dtype=torch.uint8, device="cuda:0")
+    d_cp = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    w = gpu_lib.OFWorker(W, H, device_ptrs=True, max_batch=4)
+    w.prime(d_in[0])
+    w.step_batch(d_in[1:], mask=d_mask, compressed=d_cp)
+    w.sync()
+    ref = oracle_lib.OracleOF(W, H)
+    ref.prime(frames[0])
+    for t in range(1, n):
+        rmask, rcp, _ = ref.step(frames[t])
+        assert np.array_equal(d_mask[t - 1].cpu().numpy(), rmask), t
+        assert np.array_equal(d_cp[t - 1].cpu().numpy(), rcp), t
+    w.close()
+
+
+@pytest.mark.parametrize("density", [0.0, 0.002, 0.05, 1.0])
+def test_of_compress_arbitrary_mask(gpu_lib, oracle_lib, density):
+    """compress_with_motion (of:151-183) with a decoded-style mask of any content."""
+    rng = np.random.default_rng(int(density * 1000) + 3)
+    H, W = 120, 200
+    bgr = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    mask = (rng.random((H, W)) < density).astype(np.uint8) * rng.integers(1, 256, (H, W), dtype=np.uint8)
+    got = gpu_lib._native.of_compress(bgr, mask, 100.0)
+    want = oracle_lib.of_compress(bgr, mask, 100.0)
+    assert np.array_equal(got, want)
+
+
+def test_of_rejects_unsupported(gpu_lib):
+    with pytest.raises(gpu_lib._native.DvcError):
+        gpu_lib.OFWorker(642, 360)          # not a multiple of 8
+    with pytest.raises(gpu_lib._native.DvcError):
+        gpu_lib.OFWorker(640, 360, morph_kernel=3)
+    w = gpu_lib.OFWorker(160, 96)
+    with pytest.raises(gpu_lib._native.DvcError):
+        w.step(np.zeros((96, 160, 3), np.uint8))   # step before prime
+    w.close()
