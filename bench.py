@@ -2,6 +2,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python bench.py --width 3840 --height 2160       # configs[2]: 4K FD feed
+    python bench.py --path of                        # configs[4]: 1080p OF (Farneback) path
 
 Workload (BASELINE.json configs[1]): one synthetic 1920x1080 camera feed per
 GPU (seed = rank), the full per-frame worker of frame_differencing.py:91-133 —
@@ -22,6 +24,11 @@ Extra JSON fields: ``roofline`` for the dominant kernel (k_out: hipEvent time
 per launch on the back stream, in a second pass of the same steps) and
 ``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
 feed; rank 0 at N=1 only).
+
+``--path of`` runs the fused optical-flow worker of motion_compression_opt.py
+(of:65-101 + of:141-185: gray, Farneback 3-level pyramid, vote, close/open,
+rectangles, 8x8 three-channel compression) on the same device-resident
+sequence; its dominant kernel is k_flow at pyramid level 0.
 """
 from __future__ import annotations
 
@@ -41,29 +48,36 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BACK_BYTES_PER_PX_FRAME = 9.125
 BACK_BYTES_PER_PX_LAUNCH = 0
 PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 read, new gray 1 written
+# OF: k_flow at level 0, per pixel per launch (iterations = 2): read R(prev) 20 + R(cur) 20
+# (+ flow in 8 on the 2nd), write flow 8 on the 1st / the motion bit 1/8 on the 2nd
+OF_FLOW_BYTES_PER_PX = (48.0 + 48.125) / 2
+OF_PIPE_BYTES_PER_PX = 11.25   # SURVEY.md §8d (config 5): frame I/O + state, not Farneback scratch
 
 
 def pingpong(n: int):
     return list(range(n)) + list(range(n - 2, 0, -1))
 
 
-def pmc_traffic(path: str, kernel_prefix: str):
-    """HBM bytes per launch of a kernel from a committed rocprofv3 PMC summary, or None."""
+def pmc_traffic(path: str, kernel_prefix: str, workload: str, frames_per_launch: float):
+    """HBM bytes per launch of a kernel from a committed rocprofv3 PMC summary of
+    the same workload and launch size (tools/profile_round.sh), or None."""
     try:
         with open(path) as f:
             d = json.load(f)
+        if d.get("workload") != workload or abs(d.get("frames_per_launch", frames_per_launch) - frames_per_launch) > 0.5:
+            return None
         k = d["kernels"][kernel_prefix]
         return float(k["hbm_bytes_per_launch"])
     except Exception:
         return None
 
 
-def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int):
+def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path: str = "fd"):
     import oracle  # checker / CPU baseline only
     from dvc_amd.synthetic import SyntheticClip
     oracle.build()
     clip = SyntheticClip(width, height, seed=0)
-    o = oracle.OracleFD(width, height)
+    o = oracle.OracleFD(width, height) if path == "fd" else oracle.OracleOF(width, height)
     o.prime(clip.frame(0))
     frames = [clip.frame(t) for t in range(1, max_frames + 1)]
     n, t0 = 0, time.perf_counter()
@@ -75,7 +89,7 @@ def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": f"C oracle (oracle/dvc_oracle.c, -O3, 1 thread) on frames 1..{n} of the same "
+            "sample": f"C oracle (oracle/{'dvc' if path == 'fd' else 'of'}_oracle.c, -O3, 1 thread) on frames 1..{n} of the same "
                       f"{width}x{height} synthetic feed (seed 0), {dt:.1f} s"}
 
 
@@ -90,7 +104,9 @@ def main():
     ap.add_argument("--noisy", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--batch", type=int, default=63, help="frames per device launch (max_batch)")
+    ap.add_argument("--path", choices=("fd", "of"), default="fd",
+                    help="fd: frame_differencing.py worker (headline); of: motion_compression_opt.py worker")
+    ap.add_argument("--batch", type=int, default=0, help="frames per device launch (max_batch; 0: 63 fd / 16 of)")
     ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
     args = ap.parse_args()
 
@@ -124,10 +140,14 @@ def main():
     ov = torch.empty_like(seq)
     cp = torch.empty_like(seq)
     torch.cuda.synchronize()
-    batch = 1 if args.per_frame else max(1, min(args.batch, P))
+    of = args.path == "of"
+    if of:   # the OF worker writes a mask plane instead of the red overlay
+        ov = torch.empty((P, H, W), dtype=torch.uint8, device=dev)
+    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else 63), P))
 
     def make_worker(ktiming=False):
-        w = dvc_amd.FDWorker(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch)
+        cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
+        w = cls(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch)
         w.prime(first)
         return w
 
@@ -182,11 +202,24 @@ def main():
 
     if rank == 0:
         avg_ms = kms / max(kn, 1)
-        bytes_per_launch = (BACK_BYTES_PER_PX_FRAME * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
+        res = f"{W}x{H}" if (W, H) != (1920, 1080) else "1080p"
+        workload = f"{args.path}_{res}_single_feed_per_gpu"
+        if of:   # kn counts level-0 k_flow launches (iterations per batch)
+            kname = "k_flow"
+            per_launch_frames = kframes * 2 / max(kn, 1)
+            bytes_per_launch = OF_FLOW_BYTES_PER_PX * W * H * per_launch_frames
+            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"), "k_flow", workload,
+                                  per_launch_frames)
+        else:
+            kname = "k_out"
+            per_launch_frames = kframes / max(kn, 1)
+            bytes_per_launch = (BACK_BYTES_PER_PX_FRAME * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
+            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out", workload,
+                                  per_launch_frames)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out")
+        pipe = OF_PIPE_BYTES_PER_PX if of else PIPE_BYTES_PER_PX
         line = {
-            "metric": METRIC,
+            "metric": METRIC if not of else "Mpixels/s (frames/s × H×W) 1080p optical-flow path; % HBM roofline",
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -198,24 +231,25 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": "fd_1080p_single_feed_per_gpu" if (W, H) == (1920, 1080) else f"fd_{W}x{H}",
+            "config": {"workload": workload, "path": "optical-flow (motion_compression_opt.py)" if of
+                       else "frame-differencing (frame_differencing.py)",
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": 1,
                        "ring_frames": R, "noisy": args.noisy,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
-                       "pipeline_bytes_per_px": PIPE_BYTES_PER_PX,
-                       "pipeline_GBps_per_gpu": round(PIPE_BYTES_PER_PX * args.steps * P * W * H / elapsed_max / 1e9, 1)},
-            "roofline": {"bound": "hbm", "kernel": "k_out", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                       "pipeline_bytes_per_px": pipe,
+                       "pipeline_GBps_per_gpu": round(pipe * args.steps * P * W * H / elapsed_max / 1e9, 1)},
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         "frames_per_launch": round(kframes / max(kn, 1), 2),
+                         "frames_per_launch": round(per_launch_frames, 2),
                          "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn},
             "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
                       "static_blocks": int(vec[4])},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120)
+            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

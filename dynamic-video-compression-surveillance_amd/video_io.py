@@ -93,6 +93,11 @@ def open_source(path: str):
         q = {k: v[0] for k, v in parse_qs(u.query).items()}
         clip = SyntheticClip(w, h, seed=int(q.get("seed", 0)), noisy=q.get("noisy", "0") in ("1", "true"))
         return _ArraySource(_SyntheticFrames(clip, int(q.get("frames", 100))), float(q.get("fps", 30)))
+    if not path.endswith(".npy") and cv2 is None:
+        # an .mp4 this package wrote without OpenCV is the .npy stream next to it
+        alt = os.path.splitext(path)[0] + ".npy"
+        if os.path.exists(alt):
+            path = alt
     if path.endswith(".npy"):
         if not os.path.exists(path):
             return _ArraySource(None, 0)
@@ -102,7 +107,8 @@ def open_source(path: str):
         if os.path.exists(meta):
             with open(meta) as f:
                 fps = float(json.load(f).get("fps", fps))
-        if arr.ndim != 4 or arr.shape[3] != 3 or arr.dtype != np.uint8:
+        # N x H x W x 3 BGR frames, or N x H x W single-channel frames (mask videos)
+        if arr.dtype != np.uint8 or not (arr.ndim == 3 or (arr.ndim == 4 and arr.shape[3] == 3)):
             return _ArraySource(None, 0)
         return _ArraySource(arr, fps)
     if cv2 is not None:

@@ -138,3 +138,46 @@ def test_pingpong_order():
     o = bench.pingpong(64)
     assert len(o) == 126 and o[0] == 0 and o[63] == 63 and o[-1] == 1
     assert all(abs(a - b) == 1 for a, b in zip(o, o[1:] + o[:1]))
+
+
+def test_of_execution_times_format(tmp_path):
+    """OF layout parsed with the reference's rules (performance_analysis.py:44-79, restated)."""
+    from dvc_amd.motion_compression_opt import write_execution_times
+    p = tmp_path / "execution_times.txt"
+    write_execution_times(p, (99, 12.3456, 0.12345), (99, 1.5, 0.01515))
+    lines = [ln.strip() for ln in open(p) if ln.strip()]
+    pat = r":\s*([\d\.]+)"
+    assert lines[0] == "Motion Detection:"
+    assert int(re.search(pat, lines[1]).group(1)) == 99
+    assert float(re.search(pat, lines[2]).group(1)) == 12.35
+    assert float(re.search(pat, lines[3]).group(1)) == 0.1235
+    ci = lines.index("Compression:")
+    assert int(re.search(pat, lines[ci + 1]).group(1)) == 99
+    assert float(re.search(pat, lines[ci + 2]).group(1)) == 1.5
+    assert float(re.search(pat, lines[ci + 3]).group(1)) == 0.0152
+    assert lines[-1] == "Total video processing time: 13.85 seconds"
+
+
+def test_of_unopenable_video_returns_zeros(tmp_path, caplog):
+    from dvc_amd.motion_compression_opt import compress_with_motion, temporal_smoothing_flow
+    with caplog.at_level("ERROR"):
+        assert temporal_smoothing_flow(str(tmp_path / "nope.npy"), str(tmp_path)) == (0, 0, 0)
+        assert compress_with_motion(str(tmp_path / "a.npy"), str(tmp_path / "b.npy"), str(tmp_path)) == (0, 0, 0)
+    assert "Unable to open video file" in caplog.text
+    assert "Unable to open input video" in caplog.text
+
+
+def test_gray_mask_stream_roundtrip(tmp_path):
+    """mask.mp4 without OpenCV: a single-channel .npy stream, readable by its .mp4 name."""
+    from dvc_amd import video_io
+    w = video_io.open_sink(str(tmp_path / "mask.mp4"), 25, (32, 16), is_color=False)
+    m = (np.arange(16 * 32).reshape(16, 32) % 2 * 255).astype(np.uint8)
+    w.write(m)
+    w.write(255 - m)
+    w.release()
+    src = video_io.open_source(str(tmp_path / "mask.mp4"))
+    assert src.isOpened() and src.get(video_io.CAP_PROP_FRAME_WIDTH) == 32
+    ok, f0 = src.read()
+    ok1, f1 = src.read()
+    assert ok and ok1 and np.array_equal(f0, m) and np.array_equal(f1, 255 - m)
+    assert src.read()[0] is False

@@ -166,3 +166,27 @@ def test_of_rejects_unsupported(gpu_lib):
     with pytest.raises(gpu_lib._native.DvcError):
         w.step(np.zeros((96, 160, 3), np.uint8))   # step before prime
     w.close()
+
+
+def test_process_single_video_of_dropin(gpu_lib, oracle_lib, tmp_path):
+    """motion_compression_opt.process_single_video_of on a synthetic clip: the two
+    reference passes (of:209-231) through .npy streams == the fused oracle worker."""
+    from dvc_amd import motion_compression_opt as M
+    from dvc_amd import video_io
+    from dvc_amd.synthetic import clip
+    uri = "synthetic://320x176?frames=7&seed=9"
+    M.process_single_video_of(uri, str(tmp_path))
+    out = tmp_path / "320x176"
+    frames = clip(320, 176, 7, seed=9)
+    ref = oracle_lib.OracleOF(320, 176)
+    ref.prime(frames[0])
+    ov = video_io.open_source(str(out / "overlay.mp4"))
+    mk = video_io.open_source(str(out / "mask.mp4"))
+    cp = video_io.open_source(str(out / "compressed.mp4"))
+    for t in range(1, 7):
+        rmask, rcp, _ = ref.step(frames[t])
+        assert np.array_equal(ov.read()[1], frames[t])
+        assert np.array_equal(mk.read()[1], rmask), t
+        assert np.array_equal(cp.read()[1], rcp), t
+    txt = open(out / "execution_times.txt").read()
+    assert txt.startswith("Motion Detection:\n  Frames processed: 6\n") and "Compression:\n  Frames processed: 6\n" in txt
