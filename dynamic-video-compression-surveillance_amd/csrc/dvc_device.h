@@ -41,6 +41,24 @@ __device__ __forceinline__ uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2)
     return y0 | (y1 << 8) | (y2 << 16) | (y3 << 24);
 }
 
+// The same 4 gray bytes with the v_dot4_u32_u8 unit: each coefficient split as
+// 256*hi + lo, so Y*2^14 + 2^13 = (dot4(px, hi) << 8) + dot4(px, lo) + 2^13 per
+// pixel (byte 3 of each operand is multiplied by 0); v_alignbyte puts pixel i's
+// (b, g, r) at bytes 0..2, v_perm packs the four results. Bit-identical to gray4.
+__device__ __forceinline__ uint32_t gray4_dot(uint32_t d0, uint32_t d1, uint32_t d2)
+{
+    constexpr uint32_t LO = 76u | (145u << 8) | (35u << 16);   // 1868, 9617, 4899 mod 256
+    constexpr uint32_t HI = 7u | (37u << 8) | (19u << 16);     // ... div 256
+    const uint32_t p1 = __builtin_amdgcn_alignbyte(d1, d0, 3), p2 = __builtin_amdgcn_alignbyte(d2, d1, 2);
+    const uint32_t p3 = d2 >> 8;
+    auto y = [](uint32_t p) {
+        return ((__builtin_amdgcn_udot4(p, HI, 0u, false) << 8) + __builtin_amdgcn_udot4(p, LO, 8192u, false)) >> 14;
+    };
+    const uint32_t lo = __builtin_amdgcn_perm(y(p1), y(d0), 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm(y(p3), y(p2), 0x0c0c0400u);
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
 __device__ __forceinline__ uint32_t ald(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -235,8 +253,18 @@ __device__ __forceinline__ void row_pair_unions(int W, int WW, const RowIdx& r0,
     }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// RN_f32(t / q) from one double product: d = RN53(t * RN53(1/q)) is within
+// 2^-52 (relative) of t/q, while a float quotient t/q is never a float rounding
+// midpoint (that would need 25 significant bits) and, when not equal to one,
+// lies at least 2^-49 (relative) away from it — so RN24(d) == RN24(t/q) for all
+// finite t and nonzero q. Three instructions instead of the IEEE division
+// sequence, bit-identical results.
+__device__ __forceinline__ float div_rn(float t, double qinv) { return (float)((double)t * qinv); }
+
 template <int B>
-__device__ __forceinline__ void block_dct_quant(float (&X)[B * B], const DctMat& M, float q)
+__device__ __forceinline__ void block_dct_quant(float (&X)[B * B], const DctMat& M, float q, double qinv)
 {
     float T[B * B];
     // rows: T[i][k] = sum_n X[i][n] M[k][n]
@@ -257,7 +285,7 @@ __device__ __forceinline__ void block_dct_quant(float (&X)[B * B], const DctMat&
             float t = M.m[k * B] * T[l];
 #pragma unroll
             for (int i = 1; i < B; ++i) t = __builtin_fmaf(M.m[k * B + i], T[i * B + l], t);
-            X[k * B + l] = __builtin_rintf(__fdiv_rn(t, q)) * q;
+            X[k * B + l] = __builtin_rintf(div_rn(t, qinv)) * q;
         }
     // inverse rows: T[k][n] = sum_l X[k][l] M[l][n]
 #pragma unroll
@@ -279,6 +307,82 @@ __device__ __forceinline__ void block_dct_quant(float (&X)[B * B], const DctMat&
             for (int k = 1; k < B; ++k) t = __builtin_fmaf(M.m[k * B + i], T[k * B + n], t);
             X[i * B + n] = t;
         }
+}
+
+// block_dct_quant with every dot product evaluated as before (first product,
+// then fmaf in index order) but two independent outputs per v_pk_mul_f32 /
+// v_pk_fma_f32, and the quantiser division as div_rn. Bit-identical.
+template <int B>
+__device__ __forceinline__ void block_dct_quant_pk(float (&X)[B * B], const DctMat& M, float q, double qinv)
+{
+    float T[B * B];
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int k = 0; k < B; k += 2) {
+            f32x2 t = (f32x2)(X[i * B]) * (f32x2){M.m[k * B], M.m[(k + 1) * B]};
+#pragma unroll
+            for (int n = 1; n < B; ++n)
+                t = __builtin_elementwise_fma((f32x2)(X[i * B + n]), (f32x2){M.m[k * B + n], M.m[(k + 1) * B + n]}, t);
+            T[i * B + k] = t.x;
+            T[i * B + k + 1] = t.y;
+        }
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+#pragma unroll
+        for (int l = 0; l < B; l += 2) {
+            f32x2 t = (f32x2)(M.m[k * B]) * (f32x2){T[l], T[l + 1]};
+#pragma unroll
+            for (int i = 1; i < B; ++i)
+                t = __builtin_elementwise_fma((f32x2)(M.m[k * B + i]), (f32x2){T[i * B + l], T[i * B + l + 1]}, t);
+            X[k * B + l] = __builtin_rintf(div_rn(t.x, qinv)) * q;
+            X[k * B + l + 1] = __builtin_rintf(div_rn(t.y, qinv)) * q;
+        }
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+#pragma unroll
+        for (int n = 0; n < B; n += 2) {
+            f32x2 t = (f32x2)(X[k * B]) * (f32x2){M.m[n], M.m[n + 1]};
+#pragma unroll
+            for (int l = 1; l < B; ++l)
+                t = __builtin_elementwise_fma((f32x2)(X[k * B + l]), (f32x2){M.m[l * B + n], M.m[l * B + n + 1]}, t);
+            T[k * B + n] = t.x;
+            T[k * B + n + 1] = t.y;
+        }
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int n = 0; n < B; n += 2) {
+            f32x2 t = (f32x2)(M.m[i]) * (f32x2){T[n], T[n + 1]};
+#pragma unroll
+            for (int k = 1; k < B; ++k)
+                t = __builtin_elementwise_fma((f32x2)(M.m[k * B + i]), (f32x2){T[k * B + n], T[k * B + n + 1]}, t);
+            X[i * B + n] = t.x;
+            X[i * B + n + 1] = t.y;
+        }
+}
+
+// Y (BGR2YCrCb / BGR2GRAY luma) of 4 packed BGR px as four u32, via v_dot4
+// (see gray4_dot).
+__device__ __forceinline__ void luma4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t (&y)[4])
+{
+    constexpr uint32_t LO = 76u | (145u << 8) | (35u << 16);
+    constexpr uint32_t HI = 7u | (37u << 8) | (19u << 16);
+    const uint32_t p[4] = {d0, __builtin_amdgcn_alignbyte(d1, d0, 3), __builtin_amdgcn_alignbyte(d2, d1, 2), d2 >> 8};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        y[j] = ((__builtin_amdgcn_udot4(p[j], HI, 0u, false) << 8) + __builtin_amdgcn_udot4(p[j], LO, 8192u, false)) >> 14;
+}
+
+// 4 bytes v0..v3 (low byte of each u32) -> the 3 dwords of (v0 v0 v0)(v1 v1 v1)
+// (v2 v2 v2)(v3 v3 v3) packed BGR, i.e. 4 gray pixels as BGR.
+__device__ __forceinline__ void gray_bgr4(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t* out)
+{
+    const uint32_t V = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v3, v2, 0x0c0c0400u),
+                                             __builtin_amdgcn_perm(v1, v0, 0x0c0c0400u), 0x05040100u);
+    out[0] = __builtin_amdgcn_perm(V, V, 0x01000000u);
+    out[1] = __builtin_amdgcn_perm(V, V, 0x02020101u);
+    out[2] = __builtin_amdgcn_perm(V, V, 0x03030302u);
 }
 
 __device__ __forceinline__ int descale14(int v) { return (v + 8192) >> 14; }

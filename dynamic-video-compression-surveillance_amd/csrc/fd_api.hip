@@ -354,6 +354,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.beta = h->p.beta;
     a.gamma = h->p.gamma;
     a.quant = h->p.quant;
+    a.qinv = 1.0 / (double)h->p.quant;
     {
         const float z = std::rint(std::fmaf(0.0f, h->p.alpha, std::fmaf(0.0f, h->p.beta, h->p.gamma)));
         a.acc0_fixed = z < 0.5f && z > -0.5f;  // saturate_cast<uchar>(0) == 0 (NaN/negatives excluded)

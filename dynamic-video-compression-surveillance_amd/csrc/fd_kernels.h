@@ -77,6 +77,7 @@ struct BackArgs {
     int n;                  // frames in the batch
     int ksize, anchor;
     float alpha, beta, gamma, quant;
+    double qinv;            // RN53(1 / (double)quant): the quantiser division as a product (div_rn)
     int acc0_fixed;         // addWeighted(acc 0, dilated 0) == 0: zero blocks stay zero
     DctMat M;
     unsigned long long* stats;

@@ -79,6 +79,17 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 // workgroups in flight for one extra frame read per chunk.
 constexpr int FT_W = 256, FT_H = 16, FT_Q = FT_W / 4 + 2, FT_R = FT_H + 4;
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// Arithmetic per quad of 4 px (VALU-bound kernel: every op counts):
+//   gray      gray4_dot: 2 v_dot4_u32_u8 per pixel
+//   5-tap h   one v_dot4 with taps (1,4,6,4) + the 5th byte per output, on
+//             v_alignbyte windows of the gray quads
+//   5-tap v   packed u16 lanes (sums <= 16 * 4080 < 2^16), (s + 128) >> 8
+//   threshold |cur - prev| > t per u16 lane as bit 15 of d + (0x7fff - t)
+// The previous blurred gray (fd:133) stays in registers as two u16 pairs.
 __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
                                                int chunk, const uint8_t* __restrict__ gray_in,
                                                uint8_t* __restrict__ gray_out, uint64_t* __restrict__ mbits,
@@ -92,17 +103,20 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const size_t mstride = (size_t)H * WW;
     const int t_first = blockIdx.z * chunk, t_end = min(n, t_first + chunk);
     const int t_begin = blockIdx.z == 0 ? 0 : t_first - 1;   // warm-up frame for c > 0
+    const u16x2 bias = (u16x2)(unsigned short)(0x7fff - ithresh);   // ithresh in -1..255
 
     // Every load below is unconditional from a clamped, always-valid address
     // (the value is discarded where it is not needed): a conditional load makes
     // hipcc branch around it and drain vmcnt to 0 before the next one.
-    // previous blurred gray of this lane's 4 output rows
+    // previous blurred gray of this lane's 4 output rows, as u16 pairs
     const int xc = x + 3 < W ? x : W - 4;
-    uint32_t pv[FT_H / 4];
+    u16x2 pl[FT_H / 4], ph[FT_H / 4];
 #pragma unroll
     for (int i = 0; i < FT_H / 4; ++i) {
         const int y = min(y0 + wave + 4 * i, H - 1);
-        pv[i] = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * W + xc);
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * W + xc);
+        pl[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c010c00u));
+        ph[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c02u));
     }
     // BGR of the 20 halo rows: wave w loads rows w, w+4, ..; lane l its quad l
     // (12 contiguous bytes), lanes 0/1 also the left/right halo quads.
@@ -129,12 +143,13 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const bool fix_l = x0 == 0;
     const int qe = (W - x0) / 4 + 1;              // LDS quad index of px W
     const bool fix_r = qe < FT_Q;
+    constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
     for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int r = wave + 4 * j;
-            sg[r][lane + 1] = gray4(v0[j], v1[j], v2[j]);
-            if (lane < 2) sg[r][hq + 1] = gray4(h0[j], h1[j], h2[j]);
+            sg[r][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
+            if (lane < 2) sg[r][hq + 1] = gray4_dot(h0[j], h1[j], h2[j]);
         }
         if (fix_l || fix_r) {            // uniform per workgroup
             __syncthreads();
@@ -161,12 +176,14 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
             if (it < FT_R * 64) {
                 const int r = it >> 6, q = it & 63;
                 const uint32_t a = sg[r][q], b = sg[r][q + 1], c = sg[r][q + 2];
-                const uint32_t p[8] = {(a >> 16) & 255, a >> 24, b & 255, (b >> 8) & 255, (b >> 16) & 255, b >> 24,
-                                       c & 255, (c >> 8) & 255};
-                uint32_t h[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) h[j] = p[j] + 4 * p[j + 1] + 6 * p[j + 2] + 4 * p[j + 3] + p[j + 4];
-                sh[r][q] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+                // window bytes a2 a3 b0 b1 b2 b3 c0 c1: output j = dot(W[j..j+3], K5) + W[j+4]
+                const uint32_t D0 = __builtin_amdgcn_alignbyte(b, a, 2), D1 = __builtin_amdgcn_alignbyte(b, a, 3);
+                const uint32_t D3 = __builtin_amdgcn_alignbyte(c, b, 1), D4 = __builtin_amdgcn_alignbyte(c, b, 2);
+                const uint32_t q0 = __builtin_amdgcn_udot4(D0, K5, D1 >> 24, false);
+                const uint32_t q1 = __builtin_amdgcn_udot4(D1, K5, b >> 24, false);
+                const uint32_t q2 = __builtin_amdgcn_udot4(b, K5, D3 >> 24, false);
+                const uint32_t q3 = __builtin_amdgcn_udot4(D3, K5, D4 >> 24, false);
+                sh[r][q] = make_uint2(__builtin_amdgcn_perm(q1, q0, 0x05040100u), __builtin_amdgcn_perm(q3, q2, 0x05040100u));
             }
         }
         __syncthreads();
@@ -178,18 +195,18 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
             const uint2 a0 = sh[rr][lane], a1 = sh[rr + 1][lane], a2 = sh[rr + 2][lane], a3 = sh[rr + 3][lane],
                         a4 = sh[rr + 4][lane];
             // 16-bit lanes: sum <= 16 * 4080 = 65280, packed adds cannot carry across halves
-            const uint32_t sx = a0.x + 4 * a1.x + 6 * a2.x + 4 * a3.x + a4.x;
-            const uint32_t sy = a0.y + 4 * a1.y + 6 * a2.y + 4 * a3.y + a4.y;
-            const uint32_t g = (((sx & 0xffff) + 128) >> 8) | ((((sx >> 16) + 128) >> 8) << 8) |
-                               ((((sy & 0xffff) + 128) >> 8) << 16) | ((((sy >> 16) + 128) >> 8) << 24);
-            uint32_t nib = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int da = (g >> (8 * j)) & 255, db = (pv[i] >> (8 * j)) & 255;
-                const int d = da > db ? da - db : db - da;
-                nib |= (uint32_t)(d > ithresh) << j;
-            }
-            pv[i] = g;
+            const u16x2 sx = as_u16x2(a0.x) + as_u16x2(a4.x) + ((as_u16x2(a1.x) + as_u16x2(a3.x)) << 2) +
+                             as_u16x2(a2.x) * (u16x2)6;
+            const u16x2 sy = as_u16x2(a0.y) + as_u16x2(a4.y) + ((as_u16x2(a1.y) + as_u16x2(a3.y)) << 2) +
+                             as_u16x2(a2.y) * (u16x2)6;
+            const u16x2 gl = (sx + (u16x2)128) >> 8, gh = (sy + (u16x2)128) >> 8;
+            const u16x2 dl = __builtin_elementwise_max(gl, pl[i]) - __builtin_elementwise_min(gl, pl[i]);
+            const u16x2 dh = __builtin_elementwise_max(gh, ph[i]) - __builtin_elementwise_min(gh, ph[i]);
+            const uint32_t xl = as_u32(dl + bias) & 0x80008000u, xh = as_u32(dh + bias) & 0x80008000u;
+            const uint32_t xm = (xl >> 15) | (xh >> 13);          // px 0..3 at bits 0, 16, 2, 18
+            uint32_t nib = (xm | (xm >> 15)) & 15u;
+            pl[i] = gl;
+            ph[i] = gh;
             if (y >= H || x >= W || t < t_first) nib = 0;
             unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
             w |= __shfl_xor(w, 1, 64);
@@ -205,7 +222,9 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
 #pragma unroll
         for (int i = 0; i < FT_H / 4; ++i) {
             const int y = y0 + wave + 4 * i;
-            if (y < H && x < W) *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * W + x) = pv[i];
+            if (y < H && x < W)
+                *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * W + x) =
+                    __builtin_amdgcn_perm(as_u32(ph[i]), as_u32(pl[i]), 0x06040200u);
         }
     }
 }
@@ -709,27 +728,25 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a)
 #pragma unroll
             for (int i = 0; i < B; ++i)
 #pragma unroll
-                for (int j = 0; j < B; ++j) {
-                    const int b = (px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
-                    const int gg = (px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
-                    const int r = (px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+                for (int qd = 0; qd < B / 4; ++qd) {
                     // 1868 + 9617 + 4899 = 2^14: Y of u8 input is in 0..255, no saturation
-                    X[i * B + j] = (float)descale14(b * 1868 + gg * 9617 + r * 4899) - 128.0f;
+                    uint32_t y[4];
+                    luma4(px[i][3 * qd], px[i][3 * qd + 1], px[i][3 * qd + 2], y);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) X[i * B + 4 * qd + j] = (float)((int)y[j] - 128);
                 }
-            block_dct_quant<B>(X, a.M, a.quant);
+            if constexpr (B == 4) block_dct_quant_pk<B>(X, a.M, a.quant, a.qinv);
+            else block_dct_quant<B>(X, a.M, a.quant, a.qinv);   // B = 8: the packed form spills
 #pragma unroll
-            for (int i = 0; i < B; ++i) {
-                uint8_t ob[3 * B];
+            for (int i = 0; i < B; ++i)
 #pragma unroll
-                for (int j = 0; j < B; ++j) {
-                    float v = X[i * B + j] + 128.0f;
-                    v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
-                    ob[3 * j] = ob[3 * j + 1] = ob[3 * j + 2] = (uint8_t)(uint32_t)v;
+                for (int qd = 0; qd < B / 4; ++qd) {
+                    uint32_t u[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)   // clip to [0, 255], truncating uint8 cast
+                        u[j] = (uint32_t)__builtin_amdgcn_fmed3f(X[i * B + 4 * qd + j] + 128.0f, 0.0f, 255.0f);
+                    gray_bgr4(u[0], u[1], u[2], u[3], &cw[i][3 * qd]);
                 }
-#pragma unroll
-                for (int d = 0; d < 3 * B / 4; ++d)
-                    cw[i][d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-            }
         } else {
 #pragma unroll
             for (int i = 0; i < B; ++i) {

@@ -383,6 +383,7 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     o.compressed = cp;
     o.ostride = ostride;
     o.quant = h->p.quant;
+    o.qinv = 1.0 / (double)h->p.quant;
     o.M = h->M;
     HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->stream));
     h->a_next += n;
@@ -598,6 +599,7 @@ int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int w
         o.compressed = d_out;
         o.ostride = 3 * N;
         o.quant = quant;
+        o.qinv = 1.0 / (double)quant;
         dvc_host::dct_matrix(8, o.M.m);
         e = dvc::of_launch_out(g, b, o, 1, nullptr);
     }

@@ -95,6 +95,7 @@ struct OfOutArgs {
     uint8_t* compressed;   // nullable: frame t at compressed + t*ostride, rows of 3W
     size_t ostride;
     float quant;
+    double qinv;           // RN53(1 / (double)quant), see div_rn
     DctMat M;              // 8x8 orthonormal DCT-II basis
 };
 

@@ -711,7 +711,7 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
             for (int i = 0; i < 8; ++i)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) X[i * 8 + j] = (float)((yc[c][i][j >> 2] >> (8 * (j & 3))) & 255) - 128.0f;
-            block_dct_quant<8>(X, o.M, o.quant);
+            block_dct_quant<8>(X, o.M, o.quant, o.qinv);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 uint32_t v2[2] = {0, 0};

@@ -181,3 +181,28 @@ def test_gray_mask_stream_roundtrip(tmp_path):
     ok1, f1 = src.read()
     assert ok and ok1 and np.array_equal(f0, m) and np.array_equal(f1, 255 - m)
     assert src.read()[0] is False
+
+
+def test_div_rn_equals_ieee_division():
+    """dvc_device.h div_rn: RN_f32(t/q) == (float)((double)t * RN_f64(1/q)) — the
+    kernels' quantiser division (fd:123, of:166). Random and adversarial operands:
+    quotients next to every half-integer (where rint would flip) and next to float
+    midpoints; bit-exact against numpy's IEEE float32 division."""
+    rng = np.random.default_rng(123)
+    qs = np.array([100, 40, 3, 7, 0.7, 1e-3, 1e5, 64, 0.5, 1, 99.99, 1.0000001, 123456.7, 3.3e-5],
+                  np.float32)
+    qs = np.concatenate([qs, rng.uniform(0.01, 1000, 200).astype(np.float32),
+                         np.float32(1) + np.arange(1, 200, dtype=np.float32) * np.float32(2 ** -23)])
+    for q in qs:
+        q = np.float32(q)
+        t = np.concatenate([
+            rng.uniform(-5000, 5000, 20000).astype(np.float32),
+            (rng.uniform(-1, 1, 2000) * 1e-5).astype(np.float32),
+            # t = (k + 0.5) * q and its float neighbours: quotients straddling rint boundaries
+            ((np.arange(-60, 60) + 0.5) * q).astype(np.float32),
+        ])
+        t = np.concatenate([t, np.nextafter(t, np.float32(np.inf)), np.nextafter(t, np.float32(-np.inf))])
+        want = t / q
+        got = (t.astype(np.float64) * (1.0 / np.float64(q))).astype(np.float32)
+        assert np.array_equal(want.view(np.uint32), got.view(np.uint32)), f"q={q}"
+        assert np.array_equal(np.rint(want) * q, np.rint(got) * q)

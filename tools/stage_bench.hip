@@ -91,6 +91,7 @@ int main(int argc, char** argv)
     a.beta = 0.5f;
     a.gamma = 0.f;
     a.quant = 100.f;
+    a.qinv = 1.0 / 100.0;
     a.acc0_fixed = 1;
     for (int k = 0; k < 4; ++k)
         for (int j = 0; j < 4; ++j)
