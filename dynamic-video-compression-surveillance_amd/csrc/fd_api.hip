@@ -107,7 +107,7 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 // Contour-filter scratch of one batch in flight (max_batch frames).
 struct Slot {
     dvc::CclBufs c{};
-    uint64_t *rbits = nullptr, *sbits = nullptr;   // k_acc -> k_out bits
+    uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;   // k_dilate -> k_acc -> k_out bits
     hipEvent_t ev_ccl = nullptr, ev_back = nullptr;
     bool recorded = false;  // ev_back holds a batch that the next user of the slot must wait for
 };
@@ -149,7 +149,7 @@ static void free_all(dvc_fd* h)
 {
     for (Slot& s : h->slot) {
         void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE,
-                       s.rbits, s.sbits};
+                       s.dblk, s.rblk, s.sbits};
         for (void* p : dev)
             if (p) (void)hipFree(p);
         for (hipEvent_t e : {s.ev_ccl, s.ev_back})
@@ -255,7 +255,9 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
                            (void**)&s.c.area2, (void**)&s.c.kbits};
         for (int i = 0; i < 10; ++i)
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&s.rbits, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        // block fields: (W/B)(H/B) x B*B bits = W*H/8 bytes per frame <= 8*H*WW
+        if ((e = dalloc(&s.dblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = dalloc(&s.rblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         for (hipEvent_t* ev : {&s.ev_ccl, &s.ev_back})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
@@ -343,7 +345,8 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.opitch = 3 * h->p.width;
     a.ostride = ostride;
     a.kbits = S.c.kbits;
-    a.rbits = S.rbits;
+    a.dblk = S.dblk;
+    a.rblk = S.rblk;
     a.sbits = S.sbits;
     a.SW = h->SW;
     a.sstride = h->sstride;

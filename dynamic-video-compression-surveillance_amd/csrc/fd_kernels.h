@@ -70,7 +70,8 @@ struct BackArgs {
     int opitch;
     size_t ostride;
     const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
-    uint64_t* rbits;        // acc > 127 per pixel, H x WW per frame (k_acc -> k_out)
+    void* dblk;             // dilated mask, block-major BxB bit fields per frame (k_dilate -> k_acc)
+    void* rblk;             // acc > 127 per pixel, block-major BxB bit fields per frame (k_acc -> k_out)
     uint64_t* sbits;        // acc all zero per block, (H/B) x SW per frame (k_acc -> k_out)
     int SW;                 // 64-block words per block row = ceil(W/B/64)
     size_t sstride;         // (H/B) * SW
@@ -92,7 +93,7 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
                         uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
 int band_rows(const RowGeom& g);
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
-// k_acc then k_out; `mid` (nullable) is recorded between them
+// k_dilate, k_acc, then k_out; `mid` (nullable) is recorded before k_out
 hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t mid);
 
 }  // namespace dvc

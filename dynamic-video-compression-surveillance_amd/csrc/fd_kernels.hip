@@ -495,164 +495,162 @@ __global__ void __launch_bounds__(64) k_area(CclBufs cb, RowGeom g)
 
 // ------------------------------------------------------------------- back ---
 // The back of the loop is split at its only recurrence:
-//   k_acc  (sequential over the batch's frames, per tile) 7x7 dilate of the
-//          kept mask (fd:106) and the accumulated-mask update (fd:107) with
-//          acc in registers; per frame it emits only bits: acc > 127 per pixel
-//          (rbits, the overlay's red mask, fd:110) and "acc all zero" per
-//          block (sbits, fd:117)
-//   k_out  (one grid over tiles x frames, no recurrence) red overlay
-//          (fd:110-111) and the static-block DCT quantisation with the YCrCb
-//          round trip (fd:115-130) from the BGR frame and those bits
-//
-// k_acc tile: one wave = 64 blocks across (64*B px) x 1 block row (B rows);
-// kept-mask window rows [y0-anchor, y0+B-1+ksize-1-anchor], words
-// [x0/64-1, x0/64+B] in LDS. The windows are loaded 8 frames per burst, the
-// next burst in flight while the current one is processed.
-template <int B, int KIT, int KMAX>
+//   k_dilate (tiles x frames, no recurrence) k x k dilation of the kept mask
+//          (fd:106) -> block-major bits: one BxB bit field per block
+//   k_acc  (frames in order, one lane per BxB block, no LDS / barriers) the
+//          accumulated-mask update (fd:107) with acc in registers; per frame it
+//          emits only bits: acc > 127 per pixel as the block's bit field (the
+//          overlay's red mask, fd:110) and "acc all zero" per block (fd:117)
+//   k_out  (tiles x frames, no recurrence) red overlay (fd:110-111) and the
+//          static-block DCT quantisation with the YCrCb round trip
+//          (fd:115-130) from the BGR frame and those bits
+// Block-major bit field of a BxB block: bit B*i + j = row i, column j (u16 for
+// B = 4, u64 for B = 8); frame t's fields are dense at t * (H/B) * (W/B).
+template <int B> struct BlkT;
+template <> struct BlkT<4> { typedef uint16_t T; };
+template <> struct BlkT<8> { typedef uint64_t T; };
+
+// One lane per (64-px word column, block row) of frame blockIdx.y: the B + k - 1
+// kept-mask rows it needs (out-of-image rows are skipped = ignored, as OpenCV's
+// dilate border), dilated horizontally by shifts across the neighbour words
+// (out bit x = OR of src bits x - anchor .. x + k - 1 - anchor), ORed into the
+// B output rows, then transposed into the 64/B block fields of the word.
+template <int B>
+__global__ void __launch_bounds__(256) k_dilate(BackArgs a)
+{
+    typedef typename BlkT<B>::T BT;
+    const int W = a.g.W, H = a.g.H, WW = a.g.WW, NBX = W / B;
+    const int NBY = H / B;
+    const int idx = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y;
+    if (idx >= WW * NBY) return;
+    const int wi = idx % WW, by = idx / WW, y0 = by * B;
+    const int k = a.ksize, an = a.anchor;
+    const uint64_t* kb = a.kbits + (size_t)t * H * WW;
+    uint64_t out[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) out[i] = 0;
+    for (int r = 0; r < B + k - 1; ++r) {
+        const int y = y0 - an + r;
+        if (y < 0 || y >= H) continue;
+        const uint64_t* row = kb + (size_t)y * WW;
+        const uint64_t c = row[wi], pv = wi > 0 ? row[wi - 1] : 0ull, nv = wi + 1 < WW ? row[wi + 1] : 0ull;
+        uint64_t o = c;
+        for (int off = 1; off <= k - 1 - an; ++off) o |= (c >> off) | (nv << (64 - off));
+        for (int off = 1; off <= an; ++off) o |= (c << off) | (pv >> (64 - off));
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            if (r - i >= 0 && r - i < k) out[i] |= o;
+    }
+    if (a.dbg_dil && t == a.n - 1) {
+#pragma unroll
+        for (int i = 0; i < B; ++i) a.dbg_dil[(size_t)(y0 + i) * WW + wi] = out[i];
+    }
+    BT* db = reinterpret_cast<BT*>(a.dblk) + (size_t)t * NBY * NBX + (size_t)by * NBX;
+    constexpr int PER = 64 / B;
+    const int nb = min(PER, NBX - wi * PER);
+#pragma unroll
+    for (int b = 0; b < PER; ++b) {
+        uint64_t f = 0;
+#pragma unroll
+        for (int i = 0; i < B; ++i) f |= ((out[i] >> (B * b)) & ((1ull << B) - 1)) << (B * i);
+        if (b < nb) db[wi * PER + b] = (BT)f;
+    }
+}
+
+// One lane per BxB block (64 blocks across per wave, one block row), frames in
+// order with the block's acc bytes in registers; the block fields of 8 frames
+// are loaded one chunk ahead.
+template <int B>
 __global__ void __launch_bounds__(64) k_acc(BackArgs a)
 {
-    constexpr int NWD = B + 2, MAXR = B + KMAX - 1;   // KMAX >= ksize
-    __shared__ unsigned long long s_k[MAXR][NWD];   // kept mask window
-    __shared__ unsigned long long s_h[MAXR][B];     // horizontally dilated
-    __shared__ unsigned long long s_v[B][B];        // dilated
+    typedef typename BlkT<B>::T BT;
+    constexpr BT ROWM = (BT)((1u << B) - 1);
     const int lane = threadIdx.x;
-    const int x0 = blockIdx.x * 64 * B, y0 = blockIdx.y * B;
-    const int k = a.ksize, an = a.anchor, NR = B + k - 1;
-    const int wx0 = (x0 >> 6) - 1;
-    const int W = a.g.W, H = a.g.H, WW = a.g.WW;
-    const size_t kstride = (size_t)H * WW;
-
-    size_t koff[KIT];
-    bool kok[KIT];
-#pragma unroll
-    for (int i = 0; i < KIT; ++i) {
-        const int idx = lane + 64 * i, r = idx / NWD, c = idx - r * NWD, gy = y0 - an + r, gw = wx0 + c;
-        kok[i] = idx < NR * NWD && gy >= 0 && gy < H && gw >= 0 && gw < WW;
-        koff[i] = (size_t)clampi(gy, 0, H - 1) * WW + clampi(gw, 0, WW - 1);
-    }
-    const int bx = x0 + lane * B;
-    const bool active = bx < W;
-    const int bxc = min(bx, W - B);
+    const int W = a.g.W, H = a.g.H, NBX = W / B, NBY = H / B;
+    const int bxi = blockIdx.x * 64 + lane, by = blockIdx.y;
+    const bool active = bxi < NBX;
+    const int bxc = min(bxi, NBX - 1);
+    const size_t blk = (size_t)by * NBX + bxc, NB = (size_t)NBY * NBX;
+    const int x0 = bxc * B, y0 = by * B;
     uint32_t acv[B][B / 4];
 #pragma unroll
     for (int i = 0; i < B; ++i) {
-        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(y0 + i) * W + bxc);
+        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(y0 + i) * W + x0);
 #pragma unroll
         for (int d = 0; d < B / 4; ++d) acv[i][d] = ac[d];
     }
-    // kept-mask windows of U frames per load burst, two bursts in flight
-    constexpr int U = KIT >= 8 ? 1 : 8 / KIT;
-    unsigned long long kA[U][KIT], kB[U][KIT];
-    auto load_chunk = [&](int t0, unsigned long long (&dst)[U][KIT]) {
+    const BT* db = reinterpret_cast<const BT*>(a.dblk);
+    BT* rb = reinterpret_cast<BT*>(a.rblk);
+    constexpr int U = 8;
+    BT dA[U], dB[U];
+    auto load_chunk = [&](int t0, BT (&dst)[U]) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t* kb = a.kbits + (size_t)min(t0 + u, a.n - 1) * kstride;   // clamped: unconditional
-#pragma unroll
-            for (int i = 0; i < KIT; ++i) dst[u][i] = kb[koff[i]];
-        }
+        for (int u = 0; u < U; ++u) dst[u] = db[(size_t)min(t0 + u, a.n - 1) * NB + blk];   // clamped: unconditional
     };
     unsigned long long nstatic = 0;
-
-    auto frame = [&](int t, const unsigned long long (&kw)[KIT]) {
+    auto frame = [&](int t, BT d) {
+        uint32_t aor = 0;
 #pragma unroll
-        for (int i = 0; i < KIT; ++i) {
-            const int idx = lane + 64 * i;
-            if (idx < NR * NWD) s_k[idx / NWD][idx % NWD] = kok[i] ? kw[i] : 0ull;
-        }
-        __syncthreads();
-        // horizontal dilation: out bit x = OR src bits x-an .. x+k-1-an
-        for (int i = lane; i < NR * B; i += 64) {
-            const int r = i / B, c = i % B + 1;
-            const uint64_t pv = s_k[r][c - 1], cv = s_k[r][c], nv = s_k[r][c + 1];
-            uint64_t o = 0;
-            for (int off = -an; off <= k - 1 - an; ++off) {
-                if (off == 0) o |= cv;
-                else if (off > 0) o |= (cv >> off) | (nv << (64 - off));
-                else o |= (cv << -off) | (pv >> (64 + off));
-            }
-            s_h[r][c - 1] = o;
-        }
-        __syncthreads();
-        if (lane < B * B) {
-            const int rr = lane / B, c = lane % B;
-            uint64_t o = 0;
-            for (int j = 0; j < k; ++j) o |= s_h[rr + j][c];
-            s_v[rr][c] = o;
-        }
-        __syncthreads();
-        if (a.dbg_dil && t == a.n - 1 && lane < B * B) {
-            const int rr = lane / B, c = lane % B, gw = (x0 >> 6) + c;
-            if (gw < WW) a.dbg_dil[(size_t)(y0 + rr) * WW + gw] = s_v[rr][c];
-        }
-        uint32_t dwv[B], dor = 0, aor = 0;
+        for (int i = 0; i < B; ++i)
 #pragma unroll
-        for (int i = 0; i < B; ++i) {
-            dwv[i] = (uint32_t)(s_v[i][(lane * B) >> 6] >> ((lane * B) & 63)) & ((1u << B) - 1);
-            dor |= dwv[i];
-#pragma unroll
-            for (int d = 0; d < B / 4; ++d) aor |= acv[i][d];
-        }
+            for (int q = 0; q < B / 4; ++q) aor |= acv[i][q];
         // addWeighted (fd:107); an all-zero block with no dilated pixel stays all
         // zero when addWeighted(0, 0) = 0 (a.acc0_fixed), skipping the float math
         bool zero = true;
-        if (!(a.acc0_fixed && dor == 0 && aor == 0)) {
+        if (!(a.acc0_fixed && d == 0 && aor == 0)) {
 #pragma unroll
-            for (int i = 0; i < B; ++i)
+            for (int i = 0; i < B; ++i) {
+                const uint32_t dw = (uint32_t)((d >> (B * i)) & ROWM);
 #pragma unroll
-                for (int d = 0; d < B / 4; ++d) {
-                    uint32_t av = acv[i][d], nv = 0;
+                for (int q = 0; q < B / 4; ++q) {
+                    uint32_t av = acv[i][q], nv = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const float dil = (float)(((dwv[i] >> (4 * d + j)) & 1u) ? 255 : 0);
+                        const float dil = (float)(((dw >> (4 * q + j)) & 1u) ? 255 : 0);
                         const float tv = __builtin_fmaf((float)((av >> (8 * j)) & 255), a.alpha,
                                                         __builtin_fmaf(dil, a.beta, a.gamma));
                         const float rr = __builtin_rintf(tv);
                         const uint32_t v = rr < 0.f ? 0u : (rr > 255.f ? 255u : (uint32_t)rr);
                         nv |= v << (8 * j);
                     }
-                    acv[i][d] = nv;
+                    acv[i][q] = nv;
                     zero = zero && nv == 0;
                 }
-        }
-        // bits out: acc > 127 per pixel, all-zero per block
-        uint64_t* rb = a.rbits + (size_t)t * kstride;
-        constexpr int LPW = 64 / B;   // lanes per 64-px word
-#pragma unroll
-        for (int i = 0; i < B; ++i) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int d = 0; d < B / 4; ++d) {
-                const uint32_t hb = acv[i][d] & 0x80808080u;   // bit 7 of each byte
-                m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * d);
             }
-            unsigned long long w = (unsigned long long)(active ? m : 0u) << (B * (lane % LPW));
-#pragma unroll
-            for (int sft = 1; sft < LPW; sft <<= 1) w |= __shfl_xor(w, sft, 64);
-            const int wi = (x0 >> 6) + lane / LPW;
-            if (lane % LPW == 0 && wi < WW) rb[(size_t)(y0 + i) * WW + wi] = w;
         }
+        // bits out: acc > 127 per pixel (bit 7 of each byte), all-zero per block
+        BT r = 0;
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+#pragma unroll
+            for (int q = 0; q < B / 4; ++q) {
+                const uint32_t hb = acv[i][q] & 0x80808080u;
+                const uint32_t m = ((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u);
+                r |= (BT)((BT)m << (B * i + 4 * q));
+            }
+        if (active) rb[(size_t)t * NB + blk] = r;
         const unsigned long long sb = __ballot(active && zero);
-        if (lane == 0) a.sbits[(size_t)t * a.sstride + (size_t)blockIdx.y * a.SW + blockIdx.x] = sb;
+        if (lane == 0) a.sbits[(size_t)t * a.sstride + (size_t)by * a.SW + blockIdx.x] = sb;
         nstatic += (unsigned long long)__popcll(sb);
     };
 
-    load_chunk(0, kA);
+    load_chunk(0, dA);
     for (int t0 = 0; t0 < a.n; t0 += 2 * U) {
-        load_chunk(t0 + U, kB);
+        load_chunk(t0 + U, dB);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (t0 + u < a.n) frame(t0 + u, kA[u]);
-        load_chunk(t0 + 2 * U, kA);
+            if (t0 + u < a.n) frame(t0 + u, dA[u]);
+        load_chunk(t0 + 2 * U, dA);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (t0 + U + u < a.n) frame(t0 + U + u, kB[u]);
+            if (t0 + U + u < a.n) frame(t0 + U + u, dB[u]);
     }
 
     // the accumulated mask after frame n-1 (fd:107)
     if (active) {
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(y0 + i) * W + bx);
+            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(y0 + i) * W + x0);
 #pragma unroll
             for (int d = 0; d < B / 4; ++d) ac[d] = acv[i][d];
         }
@@ -667,7 +665,7 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a)
 {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = blockIdx.z;
-    const int W = a.g.W, H = a.g.H, WW = a.g.WW;
+    const int W = a.g.W, H = a.g.H;
     const int bx = blockIdx.x * 64 * B + lane * B, by = (blockIdx.y * 4 + wave) * B;
     if (bx >= W || by >= H) return;   // no barrier below
     const uint8_t* f = a.bgr + (size_t)t * a.fstride;
@@ -682,13 +680,13 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a)
         (a.sbits[(size_t)t * a.sstride + (size_t)(by / B) * a.SW + (bx / B >> 6)] >> ((bx / B) & 63)) & 1ull;
     // overlay (fd:110-111): (0,0,255) where acc > 127
     if (a.overlay) {
-        uint32_t red[B], rany = 0;
-        const uint64_t* rb = a.rbits + (size_t)t * H * WW;
+        typedef typename BlkT<B>::T BT;
+        const int NBX = W / B;
+        const BT rf = reinterpret_cast<const BT*>(a.rblk)[(size_t)t * (H / B) * NBX + (size_t)(by / B) * NBX + bx / B];
+        uint32_t red[B];
+        const bool rany = rf != 0;
 #pragma unroll
-        for (int i = 0; i < B; ++i) {
-            red[i] = (uint32_t)(rb[(size_t)(by + i) * WW + (bx >> 6)] >> (bx & 63)) & ((1u << B) - 1);
-            rany |= red[i];
-        }
+        for (int i = 0; i < B; ++i) red[i] = (uint32_t)(rf >> (B * i)) & ((1u << B) - 1);
         uint8_t* ovf = a.overlay + (size_t)t * a.ostride;
 #pragma unroll
         for (int i = 0; i < B; ++i) {
@@ -829,25 +827,12 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
     return hipGetLastError();
 }
 
-template <int B, int KMAX>
-static void launch_acc_k(const BackArgs& a, hipStream_t s)
-{
-    const int items = (B + a.ksize - 1) * (B + 2), kit = (items + 63) / 64;
-    dim3 grid((a.g.W + 64 * B - 1) / (64 * B), a.g.H / B);
-    if (kit <= 1) hipLaunchKernelGGL((k_acc<B, 1, KMAX>), grid, dim3(64), 0, s, a);
-    else if (kit <= 2) hipLaunchKernelGGL((k_acc<B, 2, KMAX>), grid, dim3(64), 0, s, a);
-    else if (kit <= 4) hipLaunchKernelGGL((k_acc<B, 4, KMAX>), grid, dim3(64), 0, s, a);
-    else if (kit <= 8) hipLaunchKernelGGL((k_acc<B, 8, KMAX>), grid, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((k_acc<B, 16, KMAX>), grid, dim3(64), 0, s, a);
-}
-
-// small-kernel instantiations keep k_acc's LDS (long-lived workgroups) small,
-// so the contour-filter kernels of the next batch still fit beside it
 template <int B>
 static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
 {
-    if (a.ksize <= 11) launch_acc_k<B, 11>(a, s);
-    else launch_acc_k<B, 63>(a, s);
+    const int NBY = a.g.H / B;
+    hipLaunchKernelGGL(k_dilate<B>, dim3((a.g.WW * NBY + 255) / 256, a.n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_acc<B>, dim3(a.SW, NBY), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

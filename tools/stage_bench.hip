@@ -60,8 +60,9 @@ int main(int argc, char** argv)
     for (int i = 0; i < 10; ++i) CK(hipMalloc(ptrs[i], sz[i]));
     c.stats = stats;
     const int B = 4, SW = (W / B + 63) / 64;
-    uint64_t *rbits, *sbits;
-    CK(hipMalloc(&rbits, 8 * (size_t)H * g.WW * n));
+    uint64_t *dblk, *rblk, *sbits;
+    CK(hipMalloc(&dblk, 8 * (size_t)H * g.WW * n));
+    CK(hipMalloc(&rblk, 8 * (size_t)H * g.WW * n));
     CK(hipMalloc(&sbits, 8 * (size_t)(H / B) * SW * n));
     dvc::GaussTaps kp{};
     kp.n = 25;
@@ -80,7 +81,8 @@ int main(int argc, char** argv)
     a.opitch = 3 * W;
     a.ostride = F;
     a.kbits = c.kbits;
-    a.rbits = rbits;
+    a.dblk = dblk;
+    a.rblk = rblk;
     a.sbits = sbits;
     a.SW = SW;
     a.sstride = (size_t)(H / B) * SW;
