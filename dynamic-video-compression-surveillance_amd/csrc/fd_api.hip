@@ -108,8 +108,8 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 struct Slot {
     dvc::CclBufs c{};
     uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;   // k_dilate -> k_acc -> k_out bits
-    hipEvent_t ev_ccl = nullptr, ev_back = nullptr;
-    bool recorded = false;  // ev_back holds a batch that the next user of the slot must wait for
+    hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_back = nullptr;
+    bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
 };
 
 struct dvc_fd {
@@ -117,6 +117,7 @@ struct dvc_fd {
     int device = 0;
     hipStream_t stream = nullptr;  // front + contour filter (and prime); the caller's stream if given
     bool own_stream = false;
+    hipStream_t s_front = nullptr; // blur/threshold front (previous gray), internal
     hipStream_t s_back = nullptr;  // back chain (accumulated mask), internal
     dvc::RowGeom g{};
     dvc::GaussTaps kprime{};
@@ -152,7 +153,7 @@ static void free_all(dvc_fd* h)
                        s.dblk, s.rblk, s.sbits};
         for (void* p : dev)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {s.ev_ccl, s.ev_back})
+        for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_back})
             if (e) (void)hipEventDestroy(e);
     }
     void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
@@ -163,6 +164,7 @@ static void free_all(dvc_fd* h)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->s_back) (void)hipStreamDestroy(h->s_back);
+    if (h->s_front) (void)hipStreamDestroy(h->s_front);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
 }
 
@@ -175,6 +177,7 @@ static hipError_t dalloc(T** p, size_t bytes)
 static hipError_t sync_all(dvc_fd* h)
 {
     hipError_t e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && h->s_front) e = hipStreamSynchronize(h->s_front);
     if (e == hipSuccess && h->s_back) e = hipStreamSynchronize(h->s_back);
     return e;
 }
@@ -246,6 +249,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         h->own_stream = true;
     }
     if ((e = hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipStreamCreateWithFlags(&h->s_front, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     for (Slot& s : h->slot) {
         size_t sz[10];
@@ -259,7 +263,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if ((e = dalloc(&s.dblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = dalloc(&s.rblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
-        for (hipEvent_t* ev : {&s.ev_ccl, &s.ev_back})
+        for (hipEvent_t* ev : {&s.ev_front, &s.ev_ccl, &s.ev_back})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
     struct { void** ptr; size_t bytes; } allocs[] = {
@@ -282,6 +286,13 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if ((e = hipHostMalloc((void**)&h->h_acc, N)) != hipSuccess) return bad(e, "hipHostMalloc");
     }
     if ((e = hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    // the OUTSIDE gap node of every frame slice is its own root before any
+    // k_band runs (its over-budget path may walk through it)
+    for (Slot& s : h->slot) {
+        size_t sz[10];
+        dvc::CclBufs::sizes(h->g, mb, sz);
+        if ((e = hipMemsetAsync(s.c.gpar, 0, sz[6], h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    }
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return bad(e, "hipStreamSynchronize");
     *out = h;
     return DVC_OK;
@@ -321,16 +332,22 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 }  // extern "C"
 
 // Enqueue one batch of n <= max_batch device-resident frames:
-//   stream:  [wait back(i-2)] front(i) -> contour filter(i) -> ev_ccl
-//   s_back:  [wait ev_ccl] back(i) -> ev_back
+//   s_front: [wait ccl(i-2)] front(i) -> ev_front          (previous gray in order)
+//   stream:  [wait ev_front, back(i-2)] contour filter(i) -> ev_ccl
+//   s_back:  [wait ev_ccl] back(i) -> ev_back              (accumulated mask in order)
+// so front(i+2), the contour filter of batch i+1 and the back of batch i run
+// concurrently: VALU-bound, latency-bound and HBM-bound work side by side.
 static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride)
 {
     Slot& S = h->slot[h->seq & 1];
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->stream, S.ev_back, 0));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));   // S.mbits free
     HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], S.c.mbits, h->g,
-                             h->p.ithresh, h->stream));
+                             h->p.ithresh, h->s_front));
+    HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
+    HIP_OK(hipStreamWaitEvent(h->stream, S.ev_front, 0));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->stream, S.ev_back, 0));    // S.kbits free
     HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, h->stream));
     HIP_OK(hipEventRecord(S.ev_ccl, h->stream));
     HIP_OK(hipStreamWaitEvent(h->s_back, S.ev_ccl, 0));
@@ -416,7 +433,7 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
         for (int t = 0; t < m; ++t)
             for (size_t y = 0; y < H; ++y)
                 std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->stream));
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_front));
         int rc = enqueue_batch(h, h->d_in, (int)row, 3 * N, m, ov ? h->d_ov : nullptr, cp ? h->d_cp : nullptr, 3 * N);
         if (rc) return rc;
         if (ov) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_back));
@@ -566,6 +583,7 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
     hipStream_t s = nullptr;
     hipError_t e = hipMemcpy(mbits, bits.data(), 8 * H * WW, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(stats, 0, 8 * 4 * 64);
+    if (e == hipSuccess) e = hipMemset(gpar, 0, 4 * (1 + H * (CAP + 1)));
     if (e == hipSuccess) {
         dvc::CclBufs c{mbits, fbits, rs, re, nfg, fpar, gpar, gE, area2, kept, stats};
         e = dvc::launch_ccl(c, g, 1, min_area2, s);

@@ -232,35 +232,41 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
 // ------------------------------------------------------------------- band ---
 // One workgroup per band of BH rows (one wave per row): build the row's run
 // index (start/end bit words + prefix counts, in LDS) straight from the bit
-// mask and write its runs to global, then union-find in LDS over the band's
-// runs (8-connected) and gaps (4-connected; gaps on the image border joined to
-// the OUTSIDE node), flatten, and publish every run/gap's band-local root as a
-// global id. Local ids: 0 = OUTSIDE, fg (r,k) = 1 + r*CAP + k,
-// gap (r,k) = 1 + BH*CAP + r*(CAP+1) + k. Dynamic LDS: see band_lds().
-__global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
+// mask and write its runs to global, then union-find over the band's runs
+// (8-connected) and gaps (4-connected; gaps on the image border joined to the
+// OUTSIDE node), flatten, and publish every run/gap's band-local root as a
+// global id.
+// The band's nodes are numbered compactly from its actual run counts n_r:
+// 0 = OUTSIDE, run (r,k) = 1 + roff[r] + k, gap (r,k) = 1 + RT + goff[r] + k
+// (roff / goff prefix sums of n_r / n_r + 1, RT = sum n_r) — order-preserving
+// against the global ids, so "root = smallest id" carries over. When the band
+// has more nodes than the LDS budget (`budget`, e.g. pure-noise masks), the same
+// unions run on the global parent arrays instead (monotone atomicMin links).
+// Dynamic LDS: see band_lds().
+__global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, int budget)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     const uint64_t* __restrict__ mbits = fb.mbits;
     uint16_t* __restrict__ rs = fb.rs;
     uint16_t* __restrict__ re = fb.re;
     uint32_t* __restrict__ nfg = fb.nfg;
-    uint32_t* __restrict__ fpar = fb.fpar;
-    uint32_t* __restrict__ gpar = fb.gpar;
+    uint32_t* fpar = fb.fpar;
+    uint32_t* gpar = fb.gpar;
     uint32_t* __restrict__ area2 = fb.area2;
     unsigned long long* __restrict__ stats = fb.stats;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const int WW = g.WW, W = g.W;
     uint64_t* l_st = lds;
     uint64_t* l_en = l_st + BH * WW;
-    uint32_t* lp = reinterpret_cast<uint32_t*>(l_en + BH * WW);
-    uint16_t* l_ps = reinterpret_cast<uint16_t*>(lp + BH * (2 * g.CAP + 1) + 1);
+    uint16_t* l_ps = reinterpret_cast<uint16_t*>(l_en + BH * WW);
     uint16_t* l_pe = l_ps + BH * (WW + 1);
-    __shared__ int s_n[32];
+    uint32_t* lp = reinterpret_cast<uint32_t*>(l_pe + BH * (WW + 1) + 2);   // 4-byte aligned
+    __shared__ int s_n[16], s_roff[17], s_goff[17];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int y0 = blockIdx.x * BH, y = y0 + wave;
     const bool act = y < g.H;
-    const uint32_t CAP = (uint32_t)g.CAP, FG0 = 1, GP0 = 1 + (uint32_t)BH * CAP;
-    const uint32_t base = (uint32_t)y * CAP;
+    const uint32_t CAP = (uint32_t)g.CAP;
+    const uint32_t base = (uint32_t)y * CAP, gbase = 1u + (uint32_t)y * (CAP + 1);
     uint64_t* st = l_st + wave * WW;
     uint64_t* en = l_en + wave * WW;
     uint16_t* ps = l_ps + wave * (WW + 1);
@@ -278,53 +284,94 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH)
             while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
             while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
         }
-        const bool left_bg = !(st[0] & 1ull);
-        const bool right_bg = !((en[(W - 1) >> 6] >> ((W - 1) & 63)) & 1ull);
-        for (int k = lane; k < n; k += 64) lp[FG0 + wave * CAP + k] = FG0 + wave * CAP + k;
-        for (int k = lane; k <= n; k += 64) {
-            const bool nonempty = (k == 0) ? left_bg : (k == n ? right_bg : true);
-            const bool border = y == 0 || y == g.H - 1 || k == 0 || k == n;
-            const uint32_t id = GP0 + wave * (CAP + 1) + k;
-            lp[id] = (nonempty && border) ? 0u : id;
-        }
-        if (lane == 0) s_n[wave] = n;
     }
-    if (threadIdx.x == 0) lp[0] = 0;
+    if (lane == 0) s_n[wave] = act ? n : 0;
     for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);
     if (lane == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
     __syncthreads();
-
-    // ---- phase 2: unions between the band's consecutive rows, all in LDS
-    if (act && wave + 1 < BH && y + 1 < g.H) {
-        const uint32_t f0 = FG0 + wave * CAP, f1 = f0 + CAP;
-        const uint32_t q0 = GP0 + wave * (CAP + 1), q1 = q0 + CAP + 1;
-        const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
-        row_pair_unions(W, WW, r0, n, r1,
-                        [&](int i, int j) { lunion(lp, f0 + i, f1 + j); },
-                        [&](int i, int j) { lunion(lp, q0 + i, q1 + j); });
+    if (threadIdx.x == 0) {
+        int ro = 0, go = 0;
+        for (int r = 0; r < BH; ++r) {
+            s_roff[r] = ro;
+            s_goff[r] = go;
+            ro += s_n[r];
+            go += s_n[r] + 1;
+        }
+        s_roff[BH] = ro;
+        s_goff[BH] = go;
     }
     __syncthreads();
+    const int RT = s_roff[BH];
+    const bool local = 1 + RT + s_goff[BH] <= budget;   // uniform
+    const bool left_bg = act && !(st[0] & 1ull);
+    const bool right_bg = act && !((en[(W - 1) >> 6] >> ((W - 1) & 63)) & 1ull);
+    auto border_gap = [&](int k) {
+        const bool nonempty = (k == 0) ? left_bg : (k == n ? right_bg : true);
+        return nonempty && (y == 0 || y == g.H - 1 || k == 0 || k == n);
+    };
 
-    // ---- phase 3: flatten; publish band-local roots as global ids (root = min id)
-    if (act) {
-        for (int k = lane; k < n; k += 64) {
-            const uint32_t r = lfind(lp, FG0 + wave * CAP + k) - FG0;
-            fpar[base + k] = (uint32_t)(y0 + r / CAP) * CAP + r % CAP;
-            area2[base + k] = 0;
+    if (local) {
+        const uint32_t FG = 1 + s_roff[wave], GP = 1 + RT + s_goff[wave];
+        if (act) {
+            for (int k = lane; k < n; k += 64) lp[FG + k] = FG + k;
+            for (int k = lane; k <= n; k += 64) lp[GP + k] = border_gap(k) ? 0u : GP + k;
         }
-        const uint32_t gbase = 1u + (uint32_t)y * (CAP + 1);
-        for (int k = lane; k <= n; k += 64) {
-            const uint32_t r = lfind(lp, GP0 + wave * (CAP + 1) + k);
-            uint32_t gid;
-            if (r == 0) gid = 0;
-            else {
-                const uint32_t rr = r - GP0;
-                gid = 1u + (uint32_t)(y0 + rr / (CAP + 1)) * (CAP + 1) + rr % (CAP + 1);
+        if (threadIdx.x == 0) lp[0] = 0;
+        __syncthreads();
+        // ---- phase 2: unions between the band's consecutive rows, in LDS
+        if (act && wave + 1 < BH && y + 1 < g.H) {
+            const uint32_t f1 = 1 + s_roff[wave + 1], q1 = 1 + RT + s_goff[wave + 1];
+            const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
+            row_pair_unions(W, WW, r0, n, r1,
+                            [&](int i, int j) { lunion(lp, FG + i, f1 + j); },
+                            [&](int i, int j) { lunion(lp, GP + i, q1 + j); });
+        }
+        __syncthreads();
+        // ---- phase 3: flatten; publish band-local roots as global ids
+        auto row_of = [&](const int* off, uint32_t v) {   // largest r with off[r] <= v
+            int r = 0;
+            for (int q = 1; q < BH; ++q) r = (uint32_t)off[q] <= v ? q : r;
+            return r;
+        };
+        if (act) {
+            for (int k = lane; k < n; k += 64) {
+                const uint32_t l = lfind(lp, FG + k) - 1;
+                const int rr = row_of(s_roff, l);
+                fpar[base + k] = (uint32_t)(y0 + rr) * CAP + (l - s_roff[rr]);
+                area2[base + k] = 0;
             }
-            gpar[gbase + k] = gid;
+            for (int k = lane; k <= n; k += 64) {
+                const uint32_t r = lfind(lp, GP + k);
+                uint32_t gid = 0;
+                if (r != 0) {
+                    const uint32_t l = r - 1 - RT;
+                    const int rr = row_of(s_goff, l);
+                    gid = 1u + (uint32_t)(y0 + rr) * (CAP + 1) + (l - s_goff[rr]);
+                }
+                gpar[gbase + k] = gid;
+            }
         }
-        if (lane == 0) nfg[y] = (uint32_t)n;
+    } else {
+        // over budget: identity parents in global memory, unions with atomicMin links
+        if (act) {
+            for (int k = lane; k < n; k += 64) {
+                fpar[base + k] = base + k;
+                area2[base + k] = 0;
+            }
+            for (int k = lane; k <= n; k += 64) gpar[gbase + k] = border_gap(k) ? 0u : gbase + k;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;
+        __threadfence_block();
+        __syncthreads();
+        if (act && wave + 1 < BH && y + 1 < g.H) {
+            const uint32_t b1 = base + CAP, g1 = gbase + CAP + 1;
+            const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
+            row_pair_unions(W, WW, r0, n, r1,
+                            [&](int i, int j) { uf_union(fpar, base + i, b1 + j); },
+                            [&](int i, int j) { uf_union(gpar, gbase + i, g1 + j); });
+        }
     }
+    if (act && lane == 0) nfg[y] = (uint32_t)n;
     if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
 }
 
@@ -801,24 +848,28 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
 }
 
 // LDS of one k_band workgroup: run index (2 x BH x WW u64 + 2 x BH x (WW+1)
-// u16) and the band's local parents (BH x (2 CAP + 1) + 1 u32).
-size_t band_lds(const RowGeom& g, int bh)
+// u16) and the band's local parents (`budget` u32).
+size_t band_lds(const RowGeom& g, int bh, int budget)
 {
-    return (size_t)16 * bh * g.WW + ((size_t)bh * (2 * g.CAP + 1) + 1) * 4 + (size_t)4 * bh * (g.WW + 1);
+    return (size_t)16 * bh * g.WW + (size_t)4 * bh * (g.WW + 1) + 8 + (size_t)4 * budget;
 }
 
-// Rows per band: the largest power of two <= 8 whose LDS fits.
-int band_rows(const RowGeom& g)
+constexpr int BAND_ROWS = 8;
+
+int band_rows(const RowGeom&) { return BAND_ROWS; }
+
+// Node budget of a band: what fits in 40 KB of LDS (4 workgroups of 8 waves
+// per CU), at least 1024 (128 runs per row).
+static int band_budget(const RowGeom& g)
 {
-    int bh = 8;
-    while (bh > 1 && band_lds(g, bh) > 150 * 1024) bh >>= 1;
-    return bh;
+    const long long rest = 40 * 1024 - (long long)band_lds(g, BAND_ROWS, 0);
+    return (int)std::max<long long>(1024, rest / 4);
 }
 
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s)
 {
-    const int BH = band_rows(g), nb = (g.H + BH - 1) / BH;
-    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH), s, c, g, BH);
+    const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
+    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH, budget), s, c, g, BH, budget);
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3(nb - 1, n), dim3(64), 32 * g.WW + 8 * (g.WW + 1), s, c, g, BH);
     hipLaunchKernelGGL(k_resolve, dim3(g.H, n), dim3(64), 8 * g.WW + 4 * g.CAP + 16, s, c, g);

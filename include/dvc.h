@@ -111,10 +111,11 @@ const char* dvc_last_error(void);
 int         dvc_device_count(int* count);
 
 /* Create a feed handle on `device`. `hip_stream` (a hipStream_t, may be NULL for
- * a stream owned by the handle) carries prime, the blur/threshold front and the
- * contour filter; the back (dilate/accumulate/compress) runs on a second,
- * internal stream so it overlaps the next batch's front. dvc_fd_sync waits for
- * both. Replaces the per-video setup at fd:56-82. */
+ * a stream owned by the handle) carries prime and the contour filter; the
+ * blur/threshold front and the back (dilate/accumulate/compress) run on two
+ * internal streams, so batch i+2's front, batch i+1's contour filter and batch
+ * i's back overlap. dvc_fd_sync waits for all three. Replaces the per-video
+ * setup at fd:56-82. */
 int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
 
 /* Frame 0: gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77) -> previous

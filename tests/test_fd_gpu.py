@@ -106,6 +106,26 @@ def test_contour_filter_masks(gpu_lib, oracle_lib):
             assert np.array_equal(g, r), (i, ma2, int((g != r).sum()))
 
 
+@pytest.mark.parametrize("W", [2048, 4096])
+def test_contour_filter_over_budget_bands(gpu_lib, oracle_lib, W):
+    """Bands with more runs + gaps than k_band's LDS node budget take the global
+    union-find path: alternating-pixel rows (W/2 runs each), checkerboards,
+    random dense blobs and rings across band seams, vs the oracle."""
+    rng = np.random.default_rng(W)
+    H = 48
+    m = (rng.random((H, W)) < 0.45).astype(np.uint8)
+    m[0:8, :] = 0
+    m[0:8, 0::2] = 1                      # band 0: every other pixel, 8 rows
+    m[16:24, :] = (np.indices((8, W)).sum(0) % 2).astype(np.uint8)   # checkerboard band
+    m[30:44, 100:140] = 1                 # a filled square straddling a seam ...
+    m[33:41, 110:130] = 0                 # ... with a hole (holes are filled, fd:104)
+    for ma2 in (-1, 0, 10, 1000):
+        g, gn = gpu_lib._native.contour_filter(m, ma2)
+        r, rn, _ = oracle_lib.contour_filter(m, ma2)
+        assert gn == rn, (ma2, gn, rn)
+        assert np.array_equal(g, r), (ma2, int((g != r).sum()))
+
+
 def test_contour_filter_random_sweep(gpu_lib, oracle_lib):
     rng = np.random.default_rng(5)
     for _ in range(60):

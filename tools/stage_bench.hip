@@ -58,6 +58,7 @@ int main(int argc, char** argv)
     void** ptrs[10] = {(void**)&c.mbits, (void**)&c.fbits, (void**)&c.rs, (void**)&c.re, (void**)&c.nfg,
                        (void**)&c.fpar, (void**)&c.gpar, (void**)&c.gE, (void**)&c.area2, (void**)&c.kbits};
     for (int i = 0; i < 10; ++i) CK(hipMalloc(ptrs[i], sz[i]));
+    CK(hipMemset(c.gpar, 0, sz[6]));
     c.stats = stats;
     const int B = 4, SW = (W / B + 63) / 64;
     uint64_t *dblk, *rblk, *sbits;
