@@ -119,21 +119,28 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
         ph[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c02u));
     }
     // BGR of the 20 halo rows: wave w loads rows w, w+4, ..; lane l its quad l
-    // (12 contiguous bytes), lanes 0/1 also the left/right halo quads.
+    // (12 contiguous bytes). The 2 x 20 halo quads left / right of the tile are
+    // loaded and converted once, by lanes 0..39 of wave 0 (lane 2r + side).
+    // Addresses are a uniform frame base + 32-bit per-lane offsets.
     constexpr int NR = FT_R / 4;
-    uint32_t v0[NR], v1[NR], v2[NR], h0[NR], h1[NR], h2[NR];
-    const int hq = lane == 0 ? -1 : 64;           // halo quad index of lanes 0 and 1
-    const int hx = x0 + 4 * hq;
-    const int hxc = lane < 2 && hx >= 0 && hx + 3 < W ? hx : xc;
+    uint32_t off[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) off[j] = (uint32_t)(reflect1(y0 - 2 + wave + 4 * j, H) * pitch + 3 * xc);
+    const bool halo_wave = __builtin_amdgcn_readfirstlane(wave) == 0;   // scalar branch
+    const bool halo = halo_wave && lane < 2 * FT_R;
+    const int hr = lane >> 1, hs = lane & 1;
+    const int hx = x0 + (hs ? FT_W : -4);
+    const uint32_t hoff = (uint32_t)(reflect1(y0 - 2 + min(hr, FT_R - 1), H) * pitch +
+                                     3 * (hx >= 0 && hx + 3 < W ? hx : xc));
+    uint32_t v0[NR], v1[NR], v2[NR], h0, h1, h2;
     auto load = [&](const uint8_t* f) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
-            const uint8_t* row = f + (size_t)reflect1(y0 - 2 + wave + 4 * j, H) * pitch;
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(row + 3 * xc);
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(row + 3 * hxc);
-            v0[j] = p[0]; v1[j] = p[1]; v2[j] = p[2];
-            h0[j] = q[0]; h1[j] = q[1]; h2[j] = q[2];
+            const uint3 q = *reinterpret_cast<const uint3*>(f + off[j]);
+            v0[j] = q.x; v1[j] = q.y; v2[j] = q.z;
         }
+        const uint3 q = *reinterpret_cast<const uint3*>(f + hoff);
+        h0 = q.x; h1 = q.y; h2 = q.z;
     };
     load(bgr + (size_t)t_begin * fstride);
 
@@ -146,10 +153,10 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
     for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const int r = wave + 4 * j;
-            sg[r][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
-            if (lane < 2) sg[r][hq + 1] = gray4_dot(h0[j], h1[j], h2[j]);
+        for (int j = 0; j < NR; ++j) sg[wave + 4 * j][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
+        if (halo_wave) {
+            const uint32_t gh = gray4_dot(h0, h1, h2);
+            if (halo) sg[hr][hs ? FT_Q - 1 : 0] = gh;
         }
         if (fix_l || fix_r) {            // uniform per workgroup
             __syncthreads();
@@ -208,13 +215,15 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
             pl[i] = gl;
             ph[i] = gh;
             if (y >= H || x >= W || t < t_first) nib = 0;
-            unsigned long long w = (unsigned long long)nib << (4 * (lane & 15));
-            w |= __shfl_xor(w, 1, 64);
-            w |= __shfl_xor(w, 2, 64);
-            w |= __shfl_xor(w, 4, 64);
-            w |= __shfl_xor(w, 8, 64);
+            // 8 lanes x 4 px = one 32-bit half of a mask word: OR-reduce within
+            // each group of 8 lanes with DPP (quad_perm xor 1, xor 2, row_half_mirror)
+            uint32_t w = nib << (4 * (lane & 7));
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);
+            w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);
             const int wi = (x0 >> 6) + (lane >> 4);
-            if ((lane & 15) == 0 && y < H && wi < WW && t >= t_first) mb[(size_t)y * WW + wi] = w;
+            if ((lane & 7) == 0 && y < H && wi < WW && t >= t_first)
+                reinterpret_cast<uint32_t*>(mb)[((size_t)y * WW + wi) * 2 + ((lane >> 3) & 1)] = w;
         }
     }
     // frame n-1's blurred gray becomes the previous gray of the next batch
