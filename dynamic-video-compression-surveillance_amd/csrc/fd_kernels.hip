@@ -384,25 +384,42 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
     if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
 }
 
+// The per-row contour-filter kernels (merge, resolve, area, paint) are one wave
+// per row (seam), CCL_RPW independent rows per workgroup (more resident waves
+// per CU than one-wave workgroups); each wave has its own LDS slice and only
+// synchronises with itself.
+constexpr int CCL_RPW = 4;
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__host__ __device__ constexpr size_t merge_lds_words(int WW) { return (size_t)4 * WW + (size_t)(WW + 1); }
+__host__ __device__ inline size_t resolve_lds_words(const RowGeom& g) { return (size_t)g.WW + ((size_t)4 * g.CAP + 16 + 7) / 8; }
+
 // ------------------------------------------------------------------ merge ---
 // One wave per band seam (rows b*BH-1 and b*BH): run indexes of both rows in
 // LDS, then global unions of the band roots with monotone atomicMin links.
-__global__ void __launch_bounds__(64) k_merge(CclBufs cb, RowGeom g, int BH)
+__global__ void __launch_bounds__(256) k_merge(CclBufs cb, RowGeom g, int BH)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     uint32_t* fpar = fb.fpar;
     uint32_t* gpar = fb.gpar;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const int WW = g.WW;
-    const int y = (blockIdx.x + 1) * BH - 1;
-    if (y + 1 >= g.H) return;
-    uint64_t* st = lds;
+    const int WW = g.WW, wave = threadIdx.x >> 6;
+    const int y = (blockIdx.x * CCL_RPW + wave + 1) * BH - 1;
+    if (y + 1 >= g.H) return;   // no barrier below (a wave's own LDS only)
+    uint64_t* st = lds + (size_t)wave * merge_lds_words(WW);
     uint64_t* en = st + 2 * WW;
     uint16_t* ps = reinterpret_cast<uint16_t*>(en + 2 * WW);
     uint16_t* pe = ps + 2 * (WW + 1);
     const int n0 = build_row_idx(fb.mbits + (size_t)y * WW, WW, g.W, st, en, ps, pe, nullptr);
     build_row_idx(fb.mbits + (size_t)(y + 1) * WW, WW, g.W, st + WW, en + WW, ps + WW + 1, pe + WW + 1, nullptr);
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
     const uint32_t g0 = 1u + (uint32_t)y * (g.CAP + 1), g1 = g0 + (g.CAP + 1);
     const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
@@ -414,7 +431,7 @@ __global__ void __launch_bounds__(64) k_merge(CclBufs cb, RowGeom g, int BH)
 // ------------------------------------------------------------------ paint ---
 // One wave per row: the kept (filtered) mask, fd:101-104 — every run of a kept
 // component plus the holes between its runs (drawContours FILLED).
-__global__ void __launch_bounds__(64) k_paint(CclBufs cb, RowGeom g, int64_t min_area2)
+__global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t min_area2)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     const uint16_t* __restrict__ rs = fb.rs;
@@ -424,10 +441,13 @@ __global__ void __launch_bounds__(64) k_paint(CclBufs cb, RowGeom g, int64_t min
     const uint8_t* __restrict__ gE = fb.gE;
     const uint32_t* __restrict__ area2 = fb.area2;
     uint64_t* __restrict__ kbits = fb.kbits;
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_k[];
-    const int y = blockIdx.x, lane = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_k[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int y = blockIdx.x * CCL_RPW + wave;
+    if (y >= g.H) return;   // wave-local LDS and barriers only below
+    unsigned long long* s_k = lds_k + (size_t)wave * g.WW;
     for (int w = lane; w < g.WW; w += 64) s_k[w] = 0ull;
-    __syncthreads();
+    wave_sync_lds();
     const int n = (int)nfg[y];
     const uint32_t base = (uint32_t)y * g.CAP;
     const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
@@ -438,13 +458,13 @@ __global__ void __launch_bounds__(64) k_paint(CclBufs cb, RowGeom g, int64_t min
         paint_bits(s_k, 0, g.WW, rs[base + k], e);
         if (k + 1 < n && !ge[k + 1]) paint_bits(s_k, 0, g.WW, e + 1, (int)rs[base + k + 1] - 1);
     }
-    __syncthreads();
+    wave_sync_lds();
     for (int w = lane; w < g.WW; w += 64) kbits[(size_t)y * g.WW + w] = s_k[w];
 }
 
 // ---------------------------------------------------------------- resolve ---
 // One wave per row. Dynamic LDS: CAP u32 roots + WW u64 filled row.
-__global__ void __launch_bounds__(64) k_resolve(CclBufs cb, RowGeom g)
+__global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     const uint16_t* __restrict__ rs = fb.rs;
@@ -455,15 +475,17 @@ __global__ void __launch_bounds__(64) k_resolve(CclBufs cb, RowGeom g)
     uint8_t* __restrict__ gE = fb.gE;
     const uint64_t* __restrict__ mbits = fb.mbits;
     uint64_t* __restrict__ fbits = fb.fbits;
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_r[];
-    unsigned long long* s_f = s_r;
-    uint32_t* s_root = reinterpret_cast<uint32_t*>(s_r + g.WW);
-    const int y = blockIdx.x, lane = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_r[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int y = blockIdx.x * CCL_RPW + wave;
+    if (y >= g.H) return;   // wave-local LDS and barriers only below
+    unsigned long long* s_f = lds_r + (size_t)wave * resolve_lds_words(g);
+    uint32_t* s_root = reinterpret_cast<uint32_t*>(s_f + g.WW);
     const int n = (int)nfg[y];
     const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
     for (int w = lane; w < g.WW; w += 64) s_f[w] = mbits[(size_t)y * g.WW + w];
     for (int k = lane; k < n; k += 64) s_root[k] = uf_find(fpar, base + k);
-    __syncthreads();
+    wave_sync_lds();
     for (int k = lane; k <= n; k += 64) {
         int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
         int b = k == n ? g.W - 1 : (int)rs[base + k] - 1;
@@ -479,7 +501,7 @@ __global__ void __launch_bounds__(64) k_resolve(CclBufs cb, RowGeom g)
         }
         gE[(size_t)y * (g.CAP + 1) + k] = e;
     }
-    __syncthreads();
+    wave_sync_lds();
     for (int w = lane; w < g.WW; w += 64) fbits[(size_t)y * g.WW + w] = s_f[w];
 }
 
@@ -487,7 +509,7 @@ __global__ void __launch_bounds__(64) k_resolve(CclBufs cb, RowGeom g)
 // One wave per row y; F row y+1 staged in LDS. 2*area per filled run:
 //   2*popc(F'[s..e]) - F'(s) - F'(e) + [F'(s-1)&F'(s)] + [F'(e)&F'(e+1)]
 // (F' = row y+1), split additively over the runs and holes of the filled run.
-__global__ void __launch_bounds__(64) k_area(CclBufs cb, RowGeom g)
+__global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     const uint16_t* __restrict__ rs = fb.rs;
@@ -498,12 +520,15 @@ __global__ void __launch_bounds__(64) k_area(CclBufs cb, RowGeom g)
     const uint64_t* __restrict__ fbits = fb.fbits;
     uint32_t* __restrict__ area2 = fb.area2;
     unsigned long long* __restrict__ stats = fb.stats;
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_b[];
-    const int y = blockIdx.x, lane = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_b[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int y = blockIdx.x * CCL_RPW + wave;
+    if (y >= g.H) return;   // wave-local LDS and barriers only below
+    unsigned long long* s_b = lds_b + (size_t)wave * g.WW;
     const int n = (int)nfg[y];
     const bool last = y == g.H - 1;
     for (int w = lane; w < g.WW; w += 64) s_b[w] = last ? 0ull : fbits[(size_t)(y + 1) * g.WW + w];
-    __syncthreads();
+    wave_sync_lds();
     const uint32_t base = (uint32_t)y * g.CAP;
     const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
     const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
@@ -879,11 +904,13 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
 {
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
     hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH, budget), s, c, g, BH, budget);
+    const int R = CCL_RPW, rows = (g.H + R - 1) / R;
     if (nb > 1)
-        hipLaunchKernelGGL(k_merge, dim3(nb - 1, n), dim3(64), 32 * g.WW + 8 * (g.WW + 1), s, c, g, BH);
-    hipLaunchKernelGGL(k_resolve, dim3(g.H, n), dim3(64), 8 * g.WW + 4 * g.CAP + 16, s, c, g);
-    hipLaunchKernelGGL(k_area, dim3(g.H, n), dim3(64), 8 * g.WW, s, c, g);
-    hipLaunchKernelGGL(k_paint, dim3(g.H, n), dim3(64), 8 * g.WW, s, c, g, min_area2);
+        hipLaunchKernelGGL(k_merge, dim3((nb - 1 + R - 1) / R, n), dim3(64 * R), 8 * merge_lds_words(g.WW) * R, s, c,
+                           g, BH);
+    hipLaunchKernelGGL(k_resolve, dim3(rows, n), dim3(64 * R), 8 * resolve_lds_words(g) * R, s, c, g);
+    hipLaunchKernelGGL(k_area, dim3(rows, n), dim3(64 * R), (size_t)8 * g.WW * R, s, c, g);
+    hipLaunchKernelGGL(k_paint, dim3(rows, n), dim3(64 * R), (size_t)8 * g.WW * R, s, c, g, min_area2);
     return hipGetLastError();
 }
 
