@@ -398,7 +398,6 @@ __device__ __forceinline__ void wave_sync_lds()
 }
 
 __host__ __device__ constexpr size_t merge_lds_words(int WW) { return (size_t)4 * WW + (size_t)(WW + 1); }
-__host__ __device__ inline size_t resolve_lds_words(const RowGeom& g) { return (size_t)g.WW + ((size_t)4 * g.CAP + 16 + 7) / 8; }
 
 // ------------------------------------------------------------------ merge ---
 // One wave per band seam (rows b*BH-1 and b*BH): run indexes of both rows in
@@ -428,9 +427,26 @@ __global__ void __launch_bounds__(256) k_merge(CclBufs cb, RowGeom g, int BH)
                     [&](int i, int j) { uf_union(gpar, g0 + i, g1 + j); });
 }
 
+// The per-row kernels below (paint, resolve, area) give each row a group of
+// CG = 16 lanes — 4 rows per wave, 16 per workgroup — so one wave carries four
+// independent global-memory dependency chains (the union-find walks); a row's
+// runs are strided over its 16 lanes. LDS: one mask row per group.
+constexpr int CG = 16, CG_ROWS = 4 * (64 / CG);
+
+__device__ __forceinline__ int group_incl_scan(int v)
+{
+    const int sl = threadIdx.x & (CG - 1);
+#pragma unroll
+    for (int d = 1; d < CG; d <<= 1) {
+        const int t = __shfl_up(v, d, CG);
+        if (sl >= d) v += t;
+    }
+    return v;
+}
+
 // ------------------------------------------------------------------ paint ---
-// One wave per row: the kept (filtered) mask, fd:101-104 — every run of a kept
-// component plus the holes between its runs (drawContours FILLED).
+// The kept (filtered) mask, fd:101-104 — every run of a kept component plus
+// the holes between its runs (drawContours FILLED).
 __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t min_area2)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -442,28 +458,34 @@ __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t mi
     const uint32_t* __restrict__ area2 = fb.area2;
     uint64_t* __restrict__ kbits = fb.kbits;
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_k[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int y = blockIdx.x * CCL_RPW + wave;
-    if (y >= g.H) return;   // wave-local LDS and barriers only below
-    unsigned long long* s_k = lds_k + (size_t)wave * g.WW;
-    for (int w = lane; w < g.WW; w += 64) s_k[w] = 0ull;
+    const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1);
+    const int y = blockIdx.x * CG_ROWS + slot;
+    const bool act = y < g.H;
+    unsigned long long* s_k = lds_k + (size_t)slot * g.WW;
+    if (act)
+        for (int w = sl; w < g.WW; w += CG) s_k[w] = 0ull;
     wave_sync_lds();
-    const int n = (int)nfg[y];
-    const uint32_t base = (uint32_t)y * g.CAP;
-    const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
-    for (int k = lane; k < n; k += 64) {
-        const uint32_t root = fpar[base + k];
-        if (!((int64_t)area2[root] > min_area2)) continue;  // contourArea > min_area
-        const int e = re[base + k];
-        paint_bits(s_k, 0, g.WW, rs[base + k], e);
-        if (k + 1 < n && !ge[k + 1]) paint_bits(s_k, 0, g.WW, e + 1, (int)rs[base + k + 1] - 1);
+    if (act) {
+        const int n = (int)nfg[y];
+        const uint32_t base = (uint32_t)y * g.CAP;
+        const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
+        for (int k = sl; k < n; k += CG) {
+            const uint32_t root = fpar[base + k];
+            if (!((int64_t)area2[root] > min_area2)) continue;  // contourArea > min_area
+            const int e = re[base + k];
+            paint_bits(s_k, 0, g.WW, rs[base + k], e);
+            if (k + 1 < n && !ge[k + 1]) paint_bits(s_k, 0, g.WW, e + 1, (int)rs[base + k + 1] - 1);
+        }
     }
     wave_sync_lds();
-    for (int w = lane; w < g.WW; w += 64) kbits[(size_t)y * g.WW + w] = s_k[w];
+    if (act)
+        for (int w = sl; w < g.WW; w += CG) kbits[(size_t)y * g.WW + w] = s_k[w];
 }
 
 // ---------------------------------------------------------------- resolve ---
-// One wave per row. Dynamic LDS: CAP u32 roots + WW u64 filled row.
+// Gaps whose root is OUTSIDE are E; the rest are holes: painted into the
+// filled row F = not E, and the runs either side of a hole united (the
+// component inside a hole of another joins the external one enclosing it).
 __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -476,37 +498,39 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
     const uint64_t* __restrict__ mbits = fb.mbits;
     uint64_t* __restrict__ fbits = fb.fbits;
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_r[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int y = blockIdx.x * CCL_RPW + wave;
-    if (y >= g.H) return;   // wave-local LDS and barriers only below
-    unsigned long long* s_f = lds_r + (size_t)wave * resolve_lds_words(g);
-    uint32_t* s_root = reinterpret_cast<uint32_t*>(s_f + g.WW);
-    const int n = (int)nfg[y];
-    const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
-    for (int w = lane; w < g.WW; w += 64) s_f[w] = mbits[(size_t)y * g.WW + w];
-    for (int k = lane; k < n; k += 64) s_root[k] = uf_find(fpar, base + k);
+    const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1);
+    const int y = blockIdx.x * CG_ROWS + slot;
+    const bool act = y < g.H;
+    unsigned long long* s_f = lds_r + (size_t)slot * g.WW;
+    if (act)
+        for (int w = sl; w < g.WW; w += CG) s_f[w] = mbits[(size_t)y * g.WW + w];
     wave_sync_lds();
-    for (int k = lane; k <= n; k += 64) {
-        int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
-        int b = k == n ? g.W - 1 : (int)rs[base + k] - 1;
-        uint8_t e = 1;
-        if (a <= b) {
-            uint32_t r = uf_find(gpar, gbase + k);
-            atomicMin(gpar + gbase + k, r);
-            e = r == 0;
-            if (!e) {  // a hole: interior gap, both neighbours are runs of this row
-                uf_union(fpar, s_root[k - 1], s_root[k]);
-                paint_bits(s_f, 0, g.WW, a, b);
+    if (act) {
+        const int n = (int)nfg[y];
+        const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
+        for (int k = sl; k <= n; k += CG) {
+            const int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
+            const int b = k == n ? g.W - 1 : (int)rs[base + k] - 1;
+            uint8_t e = 1;
+            if (a <= b) {
+                const uint32_t r = uf_find(gpar, gbase + k);
+                atomicMin(gpar + gbase + k, r);
+                e = r == 0;
+                if (!e) {  // a hole: interior gap, both neighbours are runs of this row
+                    uf_union(fpar, base + k - 1, base + k);
+                    paint_bits(s_f, 0, g.WW, a, b);
+                }
             }
+            gE[(size_t)y * (g.CAP + 1) + k] = e;
         }
-        gE[(size_t)y * (g.CAP + 1) + k] = e;
     }
     wave_sync_lds();
-    for (int w = lane; w < g.WW; w += 64) fbits[(size_t)y * g.WW + w] = s_f[w];
+    if (act)
+        for (int w = sl; w < g.WW; w += CG) fbits[(size_t)y * g.WW + w] = s_f[w];
 }
 
 // ------------------------------------------------------------------- area ---
-// One wave per row y; F row y+1 staged in LDS. 2*area per filled run:
+// Row y with F row y+1 staged in LDS. 2*area per filled run:
 //   2*popc(F'[s..e]) - F'(s) - F'(e) + [F'(s-1)&F'(s)] + [F'(e)&F'(e+1)]
 // (F' = row y+1), split additively over the runs and holes of the filled run.
 __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
@@ -521,57 +545,62 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
     uint32_t* __restrict__ area2 = fb.area2;
     unsigned long long* __restrict__ stats = fb.stats;
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_b[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int y = blockIdx.x * CCL_RPW + wave;
-    if (y >= g.H) return;   // wave-local LDS and barriers only below
-    unsigned long long* s_b = lds_b + (size_t)wave * g.WW;
-    const int n = (int)nfg[y];
+    const int lane = threadIdx.x & 63;
+    const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1), g0 = lane & ~(CG - 1);
+    const int y = blockIdx.x * CG_ROWS + slot;
+    const bool act = y < g.H;
+    unsigned long long* s_b = lds_b + (size_t)slot * g.WW;
     const bool last = y == g.H - 1;
-    for (int w = lane; w < g.WW; w += 64) s_b[w] = last ? 0ull : fbits[(size_t)(y + 1) * g.WW + w];
+    if (act)
+        for (int w = sl; w < g.WW; w += CG) s_b[w] = last ? 0ull : fbits[(size_t)(y + 1) * g.WW + w];
     wave_sync_lds();
-    const uint32_t base = (uint32_t)y * g.CAP;
-    const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
-    const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
     int comps = 0;
-    for (int k0 = 0; k0 < n; k0 += 64) {   // uniform trip count: the wave reduces below
-        const int k = k0 + lane;
-        const bool valid = k < n;
-        const uint32_t id = base + (valid ? k : 0);
-        uint32_t r = 0xffffffffu;
-        int c = 0;
-        if (valid) {
-            r = uf_find(fpar, id);
-            atomicMin(fpar + id, r);
-            comps += r == id;
-        }
-        if (valid && !last) {
-            int s = rs[id], e = re[id];
-            c = 2 * popc_range(b, s, e);
-            if (k == 0 || ge[k]) {
-                int bs = bit_at(b, s);
-                c -= bs;
-                if (s >= 1 && bs && bit_at(b, s - 1)) c += 1;
+    if (act) {
+        const int n = (int)nfg[y];
+        const uint32_t base = (uint32_t)y * g.CAP;
+        const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
+        const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
+        const unsigned long long gmask = 0xffffull << g0;
+        for (int k0 = 0; k0 < n; k0 += CG) {   // uniform trip count within the group: it reduces below
+            const int k = k0 + sl;
+            const bool valid = k < n;
+            const uint32_t id = base + (valid ? k : 0);
+            uint32_t r = 0xffffffffu;
+            int c = 0;
+            if (valid) {
+                r = uf_find(fpar, id);
+                atomicMin(fpar + id, r);
+                comps += r == id;
             }
-            if (k == n - 1 || ge[k + 1]) {
-                int be = bit_at(b, e);
-                c -= be;
-                if (e <= g.W - 2 && be && bit_at(b, e + 1)) c += 1;
+            if (valid && !last) {
+                int s = rs[id], e = re[id];
+                c = 2 * popc_range(b, s, e);
+                if (k == 0 || ge[k]) {
+                    int bs = bit_at(b, s);
+                    c -= bs;
+                    if (s >= 1 && bs && bit_at(b, s - 1)) c += 1;
+                }
+                if (k == n - 1 || ge[k + 1]) {
+                    int be = bit_at(b, e);
+                    c -= be;
+                    if (e <= g.W - 2 && be && bit_at(b, e + 1)) c += 1;
+                }
+                if (k + 1 < n && !ge[k + 1]) c += 2 * popc_range(b, e + 1, (int)rs[id + 1] - 1);
             }
-            if (k + 1 < n && !ge[k + 1]) c += 2 * popc_range(b, e + 1, (int)rs[id + 1] - 1);
+            // one atomic per run of lanes with the same root (a large component's
+            // runs of a row would otherwise all hit one address)
+            const uint32_t rp = __shfl_up(r, 1, CG);
+            const bool head = sl == 0 || rp != r;
+            const unsigned long long heads = __ballot(head) & gmask;
+            const unsigned long long after = heads & (lane == 63 ? 0ull : (~0ull << (lane + 1)));
+            const int seg_end = after ? __builtin_ctzll(after) - 1 : g0 + CG - 1;
+            const int incl = group_incl_scan(c);
+            const int seg = __shfl(incl, seg_end, 64) - incl + c;
+            if (head && valid && seg) atomicAdd(area2 + r, (uint32_t)seg);
         }
-        // one atomic per run of lanes with the same root (a large component's
-        // runs of a row would otherwise all hit one address)
-        const uint32_t rp = __shfl_up(r, 1, 64);
-        const bool head = lane == 0 || rp != r;
-        const unsigned long long heads = __ballot(head);
-        const unsigned long long after = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-        const int seg_end = after ? __builtin_ctzll(after) - 1 : 63;
-        const int incl = wave_incl_scan(c);
-        const int seg = __shfl(incl, seg_end, 64) - incl + c;
-        if (head && valid && seg) atomicAdd(area2 + r, (uint32_t)seg);
     }
     for (int d = 32; d >= 1; d >>= 1) comps += __shfl_xor(comps, d, 64);
-    if (lane == 0 && comps) atomicAdd(stats + STAT_SLOT(y) * 4 + 2, (unsigned long long)comps);
+    if (lane == 0 && comps) atomicAdd(stats + STAT_SLOT(blockIdx.x) * 4 + 2, (unsigned long long)comps);
 }
 
 // ------------------------------------------------------------------- back ---
@@ -908,9 +937,12 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3((nb - 1 + R - 1) / R, n), dim3(64 * R), 8 * merge_lds_words(g.WW) * R, s, c,
                            g, BH);
-    hipLaunchKernelGGL(k_resolve, dim3(rows, n), dim3(64 * R), 8 * resolve_lds_words(g) * R, s, c, g);
-    hipLaunchKernelGGL(k_area, dim3(rows, n), dim3(64 * R), (size_t)8 * g.WW * R, s, c, g);
-    hipLaunchKernelGGL(k_paint, dim3(rows, n), dim3(64 * R), (size_t)8 * g.WW * R, s, c, g, min_area2);
+    (void)rows;
+    const int grows = (g.H + CG_ROWS - 1) / CG_ROWS;
+    const size_t glds = (size_t)8 * g.WW * CG_ROWS;
+    hipLaunchKernelGGL(k_resolve, dim3(grows, n), dim3(256), glds, s, c, g);
+    hipLaunchKernelGGL(k_area, dim3(grows, n), dim3(256), glds, s, c, g);
+    hipLaunchKernelGGL(k_paint, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
     return hipGetLastError();
 }
 
