@@ -194,39 +194,52 @@ __device__ __forceinline__ int select_k(const uint64_t* b, const uint16_t* pre, 
     return lo * 64 + __builtin_ctzll(v);
 }
 
-// One wave: run index of mask row `row` (global, WW words) into LDS; returns
-// the run count; *motion (nullable) = this lane's share of the row's set pixels.
-__device__ __forceinline__ int build_row_idx(const uint64_t* row, int WW, int W, uint64_t* st, uint64_t* en,
-                                             uint16_t* ps, uint16_t* pe, unsigned long long* motion)
+// A group of CGW lanes (aligned within the wave; 64 = the whole wave): run
+// index of mask row `row` (WW words) into LDS; returns the run count;
+// *motion (nullable) = this lane's share of the row's set pixels.
+template <int CGW>
+__device__ __forceinline__ int build_row_idx_g(const uint64_t* row, int WW, int W, uint64_t* st, uint64_t* en,
+                                               uint16_t* ps, uint16_t* pe, unsigned long long* motion)
 {
-    const int lane = threadIdx.x & 63;
+    const int sl = threadIdx.x & (CGW - 1);
     int ns = 0, ne = 0;
     unsigned long long m = 0;
-    for (int b0 = 0; b0 < WW; b0 += 64) {
-        const int i = b0 + lane;
+    for (int b0 = 0; b0 < WW; b0 += CGW) {
+        const int i = b0 + sl;
         const int ic = min(i, WW - 1);
         const uint64_t w0 = row[ic], pw0 = row[max(ic - 1, 0)], nw0 = row[min(ic + 1, WW - 1)];
         const uint64_t w = i < WW ? w0 : 0, pw = i > 0 && i < WW ? pw0 : 0, nw = i + 1 < WW ? nw0 : 0;
         const uint64_t s = w & ~((w << 1) | (pw >> 63));
         const uint64_t e = w & ~((w >> 1) | (nw << 63));
         const int cs = __popcll(s), ce = __popcll(e);
-        const int is = wave_incl_scan(cs), ie = wave_incl_scan(ce);
+        int is = cs, ie = ce;
+#pragma unroll
+        for (int d = 1; d < CGW; d <<= 1) {
+            const int ts = __shfl_up(is, d, CGW), te = __shfl_up(ie, d, CGW);
+            if (sl >= d) { is += ts; ie += te; }
+        }
         if (i < WW) {
             st[i] = s;
             en[i] = e;
             ps[i] = (uint16_t)(ns + is - cs);
             pe[i] = (uint16_t)(ne + ie - ce);
         }
-        ns += __shfl(is, 63, 64);
-        ne += __shfl(ie, 63, 64);
+        ns += __shfl(is, CGW - 1, CGW);
+        ne += __shfl(ie, CGW - 1, CGW);
         m += (unsigned long long)__popcll(w);
     }
-    if (lane == 0) {
+    if (sl == 0) {
         ps[WW] = (uint16_t)ns;
         pe[WW] = (uint16_t)ne;
     }
     if (motion) *motion = m;
     return ns;
+}
+
+__device__ __forceinline__ int build_row_idx(const uint64_t* row, int WW, int W, uint64_t* st, uint64_t* en,
+                                             uint16_t* ps, uint16_t* pe, unsigned long long* motion)
+{
+    return build_row_idx_g<64>(row, WW, W, st, en, ps, pe, motion);
 }
 
 // Unions between the runs (8-connected) and the gaps (4-connected) of two

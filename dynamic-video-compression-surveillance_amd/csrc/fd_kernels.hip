@@ -384,12 +384,8 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
     if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
 }
 
-// The per-row contour-filter kernels (merge, resolve, area, paint) are one wave
-// per row (seam), CCL_RPW independent rows per workgroup (more resident waves
-// per CU than one-wave workgroups); each wave has its own LDS slice and only
-// synchronises with itself.
-constexpr int CCL_RPW = 4;
-
+// Contour-filter kernels after k_band give each row (seam) a group of lanes of
+// its own and synchronise only within the wave (each group its own LDS slice).
 __device__ __forceinline__ void wave_sync_lds()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -397,34 +393,49 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ------------------------------------------------------------------ merge ---
+// One group of MG lanes per band seam (rows b*BH-1 and b*BH): run indexes of
+// both rows in LDS, then global unions of the band roots with monotone
+// atomicMin links. 64/MG seams per wave, each its own dependency chain.
+constexpr int MG = 64;   // only ~H/8 seams per frame: a whole wave each keeps enough waves in flight
+
 __host__ __device__ constexpr size_t merge_lds_words(int WW) { return (size_t)4 * WW + (size_t)(WW + 1); }
 
-// ------------------------------------------------------------------ merge ---
-// One wave per band seam (rows b*BH-1 and b*BH): run indexes of both rows in
-// LDS, then global unions of the band roots with monotone atomicMin links.
 __global__ void __launch_bounds__(256) k_merge(CclBufs cb, RowGeom g, int BH)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
     uint32_t* fpar = fb.fpar;
     uint32_t* gpar = fb.gpar;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const int WW = g.WW, wave = threadIdx.x >> 6;
-    const int y = (blockIdx.x * CCL_RPW + wave + 1) * BH - 1;
-    if (y + 1 >= g.H) return;   // no barrier below (a wave's own LDS only)
-    uint64_t* st = lds + (size_t)wave * merge_lds_words(WW);
+    const int WW = g.WW, slot = threadIdx.x / MG, sl = threadIdx.x & (MG - 1);
+    const int y = (blockIdx.x * (256 / MG) + slot + 1) * BH - 1;
+    const bool act = y + 1 < g.H;
+    uint64_t* st = lds + (size_t)slot * merge_lds_words(WW);
     uint64_t* en = st + 2 * WW;
     uint16_t* ps = reinterpret_cast<uint16_t*>(en + 2 * WW);
     uint16_t* pe = ps + 2 * (WW + 1);
-    const int n0 = build_row_idx(fb.mbits + (size_t)y * WW, WW, g.W, st, en, ps, pe, nullptr);
-    build_row_idx(fb.mbits + (size_t)(y + 1) * WW, WW, g.W, st + WW, en + WW, ps + WW + 1, pe + WW + 1, nullptr);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    int n0 = 0;
+    if (act) {
+        n0 = build_row_idx_g<MG>(fb.mbits + (size_t)y * WW, WW, g.W, st, en, ps, pe, nullptr);
+        build_row_idx_g<MG>(fb.mbits + (size_t)(y + 1) * WW, WW, g.W, st + WW, en + WW, ps + WW + 1, pe + WW + 1,
+                            nullptr);
+    }
+    wave_sync_lds();
+    if (!act) return;
     const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
     const uint32_t g0 = 1u + (uint32_t)y * (g.CAP + 1), g1 = g0 + (g.CAP + 1);
-    const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
-    row_pair_unions(g.W, WW, r0, n0, r1,
-                    [&](int i, int j) { uf_union(fpar, b0 + i, b1 + j); },
-                    [&](int i, int j) { uf_union(gpar, g0 + i, g1 + j); });
+    for (int i = sl; i < n0; i += MG) {
+        const int a = select_k(st, ps, WW, i), b = select_k(en, pe, WW, i);
+        const int j0 = rank_le(en + WW, pe + WW + 1, WW, a - 2), j1 = rank_le(st + WW, ps + WW + 1, WW, b + 1);
+        for (int j = j0; j < j1; ++j) uf_union(fpar, b0 + i, b1 + j);
+    }
+    for (int i = sl; i <= n0; i += MG) {
+        const int a = i == 0 ? 0 : select_k(en, pe, WW, i - 1) + 1;
+        const int b = i == n0 ? g.W - 1 : select_k(st, ps, WW, i) - 1;
+        if (a > b) continue;
+        const int j0 = rank_le(st + WW, ps + WW + 1, WW, a), j1 = rank_le(en + WW, pe + WW + 1, WW, b - 1);
+        for (int j = j0; j <= j1; ++j) uf_union(gpar, g0 + i, g1 + j);
+    }
 }
 
 // The per-row kernels below (paint, resolve, area) give each row a group of
@@ -933,11 +944,9 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
 {
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
     hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH, budget), s, c, g, BH, budget);
-    const int R = CCL_RPW, rows = (g.H + R - 1) / R;
     if (nb > 1)
-        hipLaunchKernelGGL(k_merge, dim3((nb - 1 + R - 1) / R, n), dim3(64 * R), 8 * merge_lds_words(g.WW) * R, s, c,
-                           g, BH);
-    (void)rows;
+        hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
+                           8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
     const int grows = (g.H + CG_ROWS - 1) / CG_ROWS;
     const size_t glds = (size_t)8 * g.WW * CG_ROWS;
     hipLaunchKernelGGL(k_resolve, dim3(grows, n), dim3(256), glds, s, c, g);
