@@ -247,17 +247,17 @@ __device__ __forceinline__ int build_row_idx(const uint64_t* row, int WW, int W,
 //   run i = [a,b] touches runs j of r1 with re1[j] >= a-1 and rs1[j] <= b+1;
 //   gap i = [a,b] overlaps gaps j of r1 with rs1[j] >= a+1 (or j = n1) and
 //   re1[j-1] <= b-1 (or j = 0).
-template <typename FG, typename BG>
+template <int CGW = 64, typename FG, typename BG>
 __device__ __forceinline__ void row_pair_unions(int W, int WW, const RowIdx& r0, int n0, const RowIdx& r1, FG fg,
                                                 BG bg)
 {
-    const int lane = threadIdx.x & 63;
-    for (int i = lane; i < n0; i += 64) {
+    const int lane = threadIdx.x & (CGW - 1);
+    for (int i = lane; i < n0; i += CGW) {
         const int a = select_k(r0.st, r0.ps, WW, i), b = select_k(r0.en, r0.pe, WW, i);
         const int j0 = rank_le(r1.en, r1.pe, WW, a - 2), j1 = rank_le(r1.st, r1.ps, WW, b + 1);
         for (int j = j0; j < j1; ++j) fg(i, j);
     }
-    for (int i = lane; i <= n0; i += 64) {
+    for (int i = lane; i <= n0; i += CGW) {
         const int a = i == 0 ? 0 : select_k(r0.en, r0.pe, WW, i - 1) + 1;
         const int b = i == n0 ? W - 1 : select_k(r0.st, r0.ps, WW, i) - 1;
         if (a > b) continue;

@@ -239,21 +239,25 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
 }
 
 // ------------------------------------------------------------------- band ---
-// One workgroup per band of BH rows (one wave per row): build the row's run
-// index (start/end bit words + prefix counts, in LDS) straight from the bit
-// mask and write its runs to global, then union-find over the band's runs
-// (8-connected) and gaps (4-connected; gaps on the image border joined to the
-// OUTSIDE node), flatten, and publish every run/gap's band-local root as a
-// global id.
+// One workgroup (256 threads) per band of BAND_ROWS = 16 rows, a group of BG =
+// 16 lanes per row: build the row's run index (start/end bit words + prefix
+// counts, in LDS) straight from the bit mask and write its runs to global,
+// then union-find over the band's runs (8-connected) and gaps (4-connected;
+// gaps on the image border joined to the OUTSIDE node), flatten, and publish
+// every run/gap's band-local root as a global id.
 // The band's nodes are numbered compactly from its actual run counts n_r:
 // 0 = OUTSIDE, run (r,k) = 1 + roff[r] + k, gap (r,k) = 1 + RT + goff[r] + k
 // (roff / goff prefix sums of n_r / n_r + 1, RT = sum n_r) — order-preserving
 // against the global ids, so "root = smallest id" carries over. When the band
 // has more nodes than the LDS budget (`budget`, e.g. pure-noise masks), the same
 // unions run on the global parent arrays instead (monotone atomicMin links).
-// Dynamic LDS: see band_lds().
-__global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, int budget)
+// Small workgroups (4 waves, <= 32 KB LDS) keep the band stage schedulable
+// beside the streaming kernels of the other two streams. Dynamic LDS: band_lds().
+constexpr int BG = 16, BAND_ROWS = 256 / BG;
+
+__global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
 {
+    constexpr int BH = BAND_ROWS;
     const CclBufs fb = cb.frame(blockIdx.y, g);
     const uint64_t* __restrict__ mbits = fb.mbits;
     uint16_t* __restrict__ rs = fb.rs;
@@ -270,33 +274,33 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
     uint16_t* l_ps = reinterpret_cast<uint16_t*>(l_en + BH * WW);
     uint16_t* l_pe = l_ps + BH * (WW + 1);
     uint32_t* lp = reinterpret_cast<uint32_t*>(l_pe + BH * (WW + 1) + 2);   // 4-byte aligned
-    __shared__ int s_n[16], s_roff[17], s_goff[17];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int y0 = blockIdx.x * BH, y = y0 + wave;
+    __shared__ int s_n[BH], s_roff[BH + 1], s_goff[BH + 1];
+    const int slot = threadIdx.x / BG, sl = threadIdx.x & (BG - 1);
+    const int y0 = blockIdx.x * BH, y = y0 + slot;
     const bool act = y < g.H;
     const uint32_t CAP = (uint32_t)g.CAP;
     const uint32_t base = (uint32_t)y * CAP, gbase = 1u + (uint32_t)y * (CAP + 1);
-    uint64_t* st = l_st + wave * WW;
-    uint64_t* en = l_en + wave * WW;
-    uint16_t* ps = l_ps + wave * (WW + 1);
-    uint16_t* pe = l_pe + wave * (WW + 1);
+    uint64_t* st = l_st + slot * WW;
+    uint64_t* en = l_en + slot * WW;
+    uint16_t* ps = l_ps + slot * (WW + 1);
+    uint16_t* pe = l_pe + slot * (WW + 1);
 
     // ---- phase 1: run index of row y in LDS; runs to global (later kernels)
     int n = 0;
     unsigned long long motion = 0;
     if (act) {
         const uint64_t* row = mbits + (size_t)y * WW;
-        n = build_row_idx(row, WW, W, st, en, ps, pe, &motion);
-        for (int i = lane; i < WW; i += 64) {
+        n = build_row_idx_g<BG>(row, WW, W, st, en, ps, pe, &motion);
+        for (int i = sl; i < WW; i += BG) {
             uint64_t s = st[i], e = en[i];
             int ks = ps[i], ke = pe[i];
             while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
             while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
         }
     }
-    if (lane == 0) s_n[wave] = act ? n : 0;
-    for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);
-    if (lane == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
+    if (sl == 0) s_n[slot] = act ? n : 0;
+    for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);   // the wave's 4 rows
+    if ((threadIdx.x & 63) == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
     __syncthreads();
     if (threadIdx.x == 0) {
         int ro = 0, go = 0;
@@ -320,20 +324,20 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
     };
 
     if (local) {
-        const uint32_t FG = 1 + s_roff[wave], GP = 1 + RT + s_goff[wave];
+        const uint32_t FG = 1 + s_roff[slot], GP = 1 + RT + s_goff[slot];
         if (act) {
-            for (int k = lane; k < n; k += 64) lp[FG + k] = FG + k;
-            for (int k = lane; k <= n; k += 64) lp[GP + k] = border_gap(k) ? 0u : GP + k;
+            for (int k = sl; k < n; k += BG) lp[FG + k] = FG + k;
+            for (int k = sl; k <= n; k += BG) lp[GP + k] = border_gap(k) ? 0u : GP + k;
         }
         if (threadIdx.x == 0) lp[0] = 0;
         __syncthreads();
         // ---- phase 2: unions between the band's consecutive rows, in LDS
-        if (act && wave + 1 < BH && y + 1 < g.H) {
-            const uint32_t f1 = 1 + s_roff[wave + 1], q1 = 1 + RT + s_goff[wave + 1];
+        if (act && slot + 1 < BH && y + 1 < g.H) {
+            const uint32_t f1 = 1 + s_roff[slot + 1], q1 = 1 + RT + s_goff[slot + 1];
             const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
-            row_pair_unions(W, WW, r0, n, r1,
-                            [&](int i, int j) { lunion(lp, FG + i, f1 + j); },
-                            [&](int i, int j) { lunion(lp, GP + i, q1 + j); });
+            row_pair_unions<BG>(W, WW, r0, n, r1,
+                                [&](int i, int j) { lunion(lp, FG + i, f1 + j); },
+                                [&](int i, int j) { lunion(lp, GP + i, q1 + j); });
         }
         __syncthreads();
         // ---- phase 3: flatten; publish band-local roots as global ids
@@ -343,13 +347,13 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
             return r;
         };
         if (act) {
-            for (int k = lane; k < n; k += 64) {
+            for (int k = sl; k < n; k += BG) {
                 const uint32_t l = lfind(lp, FG + k) - 1;
                 const int rr = row_of(s_roff, l);
                 fpar[base + k] = (uint32_t)(y0 + rr) * CAP + (l - s_roff[rr]);
                 area2[base + k] = 0;
             }
-            for (int k = lane; k <= n; k += 64) {
+            for (int k = sl; k <= n; k += BG) {
                 const uint32_t r = lfind(lp, GP + k);
                 uint32_t gid = 0;
                 if (r != 0) {
@@ -363,24 +367,24 @@ __global__ void __launch_bounds__(1024) k_band(CclBufs cb, RowGeom g, int BH, in
     } else {
         // over budget: identity parents in global memory, unions with atomicMin links
         if (act) {
-            for (int k = lane; k < n; k += 64) {
+            for (int k = sl; k < n; k += BG) {
                 fpar[base + k] = base + k;
                 area2[base + k] = 0;
             }
-            for (int k = lane; k <= n; k += 64) gpar[gbase + k] = border_gap(k) ? 0u : gbase + k;
+            for (int k = sl; k <= n; k += BG) gpar[gbase + k] = border_gap(k) ? 0u : gbase + k;
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;
         __threadfence_block();
         __syncthreads();
-        if (act && wave + 1 < BH && y + 1 < g.H) {
+        if (act && slot + 1 < BH && y + 1 < g.H) {
             const uint32_t b1 = base + CAP, g1 = gbase + CAP + 1;
             const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
-            row_pair_unions(W, WW, r0, n, r1,
-                            [&](int i, int j) { uf_union(fpar, base + i, b1 + j); },
-                            [&](int i, int j) { uf_union(gpar, gbase + i, g1 + j); });
+            row_pair_unions<BG>(W, WW, r0, n, r1,
+                                [&](int i, int j) { uf_union(fpar, base + i, b1 + j); },
+                                [&](int i, int j) { uf_union(gpar, gbase + i, g1 + j); });
         }
     }
-    if (act && lane == 0) nfg[y] = (uint32_t)n;
+    if (act && sl == 0) nfg[y] = (uint32_t)n;
     if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;  // the OUTSIDE node is its own root
 }
 
@@ -928,22 +932,19 @@ size_t band_lds(const RowGeom& g, int bh, int budget)
     return (size_t)16 * bh * g.WW + (size_t)4 * bh * (g.WW + 1) + 8 + (size_t)4 * budget;
 }
 
-constexpr int BAND_ROWS = 8;
-
 int band_rows(const RowGeom&) { return BAND_ROWS; }
 
-// Node budget of a band: what fits in 40 KB of LDS (4 workgroups of 8 waves
-// per CU), at least 1024 (128 runs per row).
+// Node budget of a band: what fits in 32 KB of LDS, at least 1024.
 static int band_budget(const RowGeom& g)
 {
-    const long long rest = 40 * 1024 - (long long)band_lds(g, BAND_ROWS, 0);
+    const long long rest = 32 * 1024 - (long long)band_lds(g, BAND_ROWS, 0);
     return (int)std::max<long long>(1024, rest / 4);
 }
 
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s)
 {
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
-    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(64 * BH), band_lds(g, BH, budget), s, c, g, BH, budget);
+    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(256), band_lds(g, BH, budget), s, c, g, budget);
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
                            8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
