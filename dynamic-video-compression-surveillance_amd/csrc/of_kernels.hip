@@ -39,7 +39,7 @@ namespace dvc {
 namespace {
 
 constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
-constexpr int FL_W = 64, FL_H = 16;   // flow tile
+constexpr int FL_W = 32, FL_H = 16;   // flow tile (32 wide: <= 26 KB LDS, 6 workgroups per CU)
 
 __device__ __forceinline__ long long ring(long long a, int n) { return ((a % n) + n) % n; }
 
@@ -149,9 +149,9 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 - PN + i, x = x0 - PN + j;
         if (y < 0 || y >= H || x < 0 || x >= W) continue;
-        const int xl = reflect101(x - 1, W) - (x0 - HG), xc = x - (x0 - HG), xr = reflect101(x + 1, W) - (x0 - HG);
+        const int xl = reflect1(x - 1, W) - (x0 - HG), xc = x - (x0 - HG), xr = reflect1(x + 1, W) - (x0 - HG);
         float hv[3];
-        const int ys[3] = {reflect101(y - 1, H), y, reflect101(y + 1, H)};
+        const int ys[3] = {reflect1(y - 1, H), y, reflect1(y + 1, H)};
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             const float* s = sg + (ys[q] - (y0 - HG)) * GW;
@@ -260,68 +260,110 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     const float* src = A.src ? A.src + (size_t)t * (A.src_mode == 1 ? (size_t)A.sw * A.sh : lvpx) * 2 : nullptr;
     static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
 
-    // ---- FarnebackUpdateMatrices over tile + halo (oc_update_matrices)
-    for (int idx = tid; idx < RH * RW; idx += 256) {
-        const int i = idx / RW, j = idx - i * RW;
-        const int y = y0 - m + i, x = x0 - m + j;
-        if (y < 0 || y >= h || x < 0 || x >= w) continue;
-        float dx = 0.f, dy = 0.f;
-        if (A.src_mode == 2) {
-            dx = src[((size_t)y * w + x) * 2];
-            dy = src[((size_t)y * w + x) * 2 + 1];
-        } else if (A.src_mode == 1) {
-            const LinTap ty = A.lv.uy[y], tx = A.lv.ux[x];
-            const float* r0 = src + (size_t)ty.s0 * A.sw * 2;
-            const float* r1 = src + (size_t)ty.s1 * A.sw * 2;
-            float v[2];
+    // ---- FarnebackUpdateMatrices over tile + halo (oc_update_matrices).
+    // Positions in groups of MQ per thread: every address is clamped into the
+    // image and every load unconditional (results of out-of-image positions
+    // are discarded), so a group's flow / R0 loads and then its bilinear R1
+    // gathers are all in flight together instead of one dependent round trip
+    // pair per position.
+    constexpr int MQ = 2;
+    const int npos = RH * RW;
+    for (int q0 = tid; q0 < npos; q0 += 256 * MQ) {
+        int idx[MQ], xs[MQ], ys[MQ];
+        bool ok[MQ];
+        float dxv[MQ], dyv[MQ], r0v[MQ][5];
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float t0 = r0[tx.s0 * 2 + c] * tx.w0 + r0[tx.s1 * 2 + c] * tx.w1;
-                const float t1 = r1[tx.s0 * 2 + c] * tx.w0 + r1[tx.s1 * 2 + c] * tx.w1;
-                v[c] = t0 * ty.w0 + t1 * ty.w1;
+        for (int u = 0; u < MQ; ++u) {
+            idx[u] = q0 + 256 * u;
+            const int i = idx[u] / RW, j = idx[u] - i * RW;
+            const int y = y0 - m + i, x = x0 - m + j;
+            ok[u] = idx[u] < npos && y >= 0 && y < h && x >= 0 && x < w;
+            ys[u] = min(max(y, 0), h - 1);
+            xs[u] = min(max(x, 0), w - 1);
+            dxv[u] = 0.f;
+            dyv[u] = 0.f;
+            if (A.src_mode == 2) {   // uniform
+                const float2 f = *reinterpret_cast<const float2*>(src + ((size_t)ys[u] * w + xs[u]) * 2);
+                dxv[u] = f.x;
+                dyv[u] = f.y;
+            } else if (A.src_mode == 1) {
+                const LinTap ty = A.lv.uy[ys[u]], tx = A.lv.ux[xs[u]];
+                const float* ra = src + (size_t)ty.s0 * A.sw * 2;
+                const float* rb = src + (size_t)ty.s1 * A.sw * 2;
+                float v[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float t0 = ra[tx.s0 * 2 + c] * tx.w0 + ra[tx.s1 * 2 + c] * tx.w1;
+                    const float t1 = rb[tx.s0 * 2 + c] * tx.w0 + rb[tx.s1 * 2 + c] * tx.w1;
+                    v[c] = t0 * ty.w0 + t1 * ty.w1;
+                }
+                dxv[u] = v[0] * g.up;
+                dyv[u] = v[1] * g.up;
             }
-            dx = v[0] * g.up;
-            dy = v[1] * g.up;
+            const float* r0 = R0 + ((size_t)ys[u] * w + xs[u]) * 5;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) r0v[u][c] = r0[c];
         }
-        const float* r0 = R0 + ((size_t)y * w + x) * 5;
-        float fx = (float)x + dx, fy = (float)y + dy;
-        const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
-        float r2, r3, r4, r5, r6;
-        fx -= (float)x1;
-        fy -= (float)y1;
-        if ((unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1)) {
-            const float* p = R1 + ((size_t)y1 * w + x1) * 5;
+        float pq[MQ][20];
+        float fxv[MQ], fyv[MQ];
+        bool inb[MQ];
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            float fx = (float)xs[u] + dxv[u], fy = (float)ys[u] + dyv[u];
+            const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
+            fxv[u] = fx - (float)x1;
+            fyv[u] = fy - (float)y1;
+            inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
+            const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
+            const float* p = R1 + ((size_t)y1c * w + x1c) * 5;
             const float* q = p + (size_t)w * 5;
-            const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
-            r2 = a00 * p[0] + a01 * p[5] + a10 * q[0] + a11 * q[5];
-            r3 = a00 * p[1] + a01 * p[6] + a10 * q[1] + a11 * q[6];
-            r4 = a00 * p[2] + a01 * p[7] + a10 * q[2] + a11 * q[7];
-            r5 = a00 * p[3] + a01 * p[8] + a10 * q[3] + a11 * q[8];
-            r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
-            r4 = (r0[2] + r4) * 0.5f;
-            r5 = (r0[3] + r5) * 0.5f;
-            r6 = (r0[4] + r6) * 0.25f;
-        } else {
-            r2 = r3 = 0.f;
-            r4 = r0[2];
-            r5 = r0[3];
-            r6 = r0[4] * 0.5f;
+#pragma unroll
+            for (int c = 0; c < 10; ++c) {
+                pq[u][c] = p[c];
+                pq[u][10 + c] = q[c];
+            }
         }
-        r2 = (r0[0] - r2) * 0.5f;
-        r3 = (r0[1] - r3) * 0.5f;
-        r2 += r4 * dy + r6 * dx;
-        r3 += r6 * dy + r5 * dx;
-        if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
-            const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
-                                (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
-            r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            if (!ok[u]) continue;
+            const int x = xs[u], y = ys[u];
+            const float dx = dxv[u], dy = dyv[u], fx = fxv[u], fy = fyv[u];
+            const float* r0 = r0v[u];
+            const float* p = pq[u];
+            const float* q = pq[u] + 10;
+            float r2, r3, r4, r5, r6;
+            if (inb[u]) {
+                const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+                r2 = a00 * p[0] + a01 * p[5] + a10 * q[0] + a11 * q[5];
+                r3 = a00 * p[1] + a01 * p[6] + a10 * q[1] + a11 * q[6];
+                r4 = a00 * p[2] + a01 * p[7] + a10 * q[2] + a11 * q[7];
+                r5 = a00 * p[3] + a01 * p[8] + a10 * q[3] + a11 * q[8];
+                r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
+                r4 = (r0[2] + r4) * 0.5f;
+                r5 = (r0[3] + r5) * 0.5f;
+                r6 = (r0[4] + r6) * 0.25f;
+            } else {
+                r2 = r3 = 0.f;
+                r4 = r0[2];
+                r5 = r0[3];
+                r6 = r0[4] * 0.5f;
+            }
+            r2 = (r0[0] - r2) * 0.5f;
+            r3 = (r0[1] - r3) * 0.5f;
+            r2 += r4 * dy + r6 * dx;
+            r3 += r6 * dy + r5 * dx;
+            if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
+                const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
+                                    (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+                r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+            }
+            float* M = sM + (size_t)idx[u] * 5;
+            M[0] = r4 * r4 + r6 * r6;
+            M[1] = (r4 + r5) * r6;
+            M[2] = r5 * r5 + r6 * r6;
+            M[3] = r4 * r2 + r6 * r3;
+            M[4] = r6 * r2 + r5 * r3;
         }
-        float* M = sM + (size_t)idx * 5;
-        M[0] = r4 * r4 + r6 * r6;
-        M[1] = (r4 + r5) * r6;
-        M[2] = r5 * r5 + r6 * r6;
-        M[3] = r4 * r2 + r6 * r3;
-        M[4] = r6 * r2 + r5 * r3;
     }
     __syncthreads();
 
@@ -359,11 +401,13 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     }
     __syncthreads();
 
-    // ---- horizontal box sums, flow = G^-1 h (oc_update_flow_box); one wave per row
+    // ---- horizontal box sums, flow = G^-1 h (oc_update_flow_box); a wave covers
+    // two 32-px rows (lanes 0-31 row i, 32-63 row i+1)
     float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
     unsigned long long nmot = 0;
-    for (int i = wave; i < FL_H; i += 4) {
-        const int y = y0 + i, x = x0 + lane;
+    for (int i2 = wave; i2 < FL_H / 2; i2 += 4) {
+        const int i = 2 * i2 + (lane >> 5);
+        const int y = y0 + i, x = x0 + (lane & 31);
         const bool act = y < h && x < w;
         float fxo = 0.f, fyo = 0.f;
         if (act) {
@@ -380,22 +424,21 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
             fyo = (float)((g22 * h1 - g12 * h2) * idet);
         }
         if (!A.last) {
-            if (act) {
-                dst[((size_t)y * w + x) * 2] = fxo;
-                dst[((size_t)y * w + x) * 2 + 1] = fyo;
-            }
+            if (act) *reinterpret_cast<float2*>(dst + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
         } else {
             // of:82-83: cartToPolar magnitude (float) > flow_threshold
             const float mag = sqrtf(fxo * fxo + fyo * fyo);
             const bool bit = act && mag > g.flow_thr;
             const unsigned long long word = __ballot(bit);
-            if (lane == 0 && y < h)
-                A.mring[(size_t)ring(a, g.RB) * h * g.WW + (size_t)y * g.WW + (x0 >> 6)] = word;
-            nmot += (unsigned long long)__popcll(word);
-            if (A.dbg_flow && t == A.n - 1 && act) {
-                A.dbg_flow[((size_t)y * w + x) * 2] = fxo;
-                A.dbg_flow[((size_t)y * w + x) * 2 + 1] = fyo;
+            uint32_t* mr = reinterpret_cast<uint32_t*>(A.mring + (size_t)ring(a, g.RB) * h * g.WW);
+            const int half = (x0 >> 5) & 1;
+            if ((lane & 31) == 0 && y < h) {
+                mr[((size_t)y * g.WW + (x0 >> 6)) * 2 + half] = (uint32_t)(word >> (lane & 32));
+                if (half == 0 && x0 + 32 >= w) mr[((size_t)y * g.WW + (x0 >> 6)) * 2 + 1] = 0u;   // no tile owns it
             }
+            nmot += (unsigned long long)__popcll(word);
+            if (A.dbg_flow && t == A.n - 1 && act)
+                *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
         }
     }
     (void)nmot;

@@ -96,6 +96,7 @@ def test_of_stages(gpu_lib, oracle_lib, W, H):
     (320, 176, 6, 2, False),     # 2 levels
     (640, 360, 5, 0, False),     # 3 levels
     (640, 360, 4, 5, True),
+    (328, 184, 4, 7, False),     # width not a multiple of 32 / 64
 ])
 def test_of_parity_synthetic(gpu_lib, oracle_lib, W, H, n, seed, noisy):
     from dvc_amd.synthetic import clip
