@@ -57,9 +57,14 @@ def process_feeds(video_paths: Iterable[str], output_dir: str, technique: str = 
     rank, world, local = dist_env()
     os.environ.setdefault("DVC_DEVICE", str(local))
     mine = shard(list(video_paths), rank, world)
-    if technique != "Frame Differencing":
-        raise NotImplementedError(f"technique {technique!r}: only the frame-differencing path is accelerated")
-    from .frame_differencing import process_single_video_fd
+    if technique == "Frame Differencing":           # windows.py:152-154
+        from .frame_differencing import process_single_video_fd as run
+    elif technique == "Optical Flow":               # windows.py:149-151
+        if kwargs:
+            raise TypeError("process_single_video_of takes no keyword arguments (of:195)")
+        from .motion_compression_opt import process_single_video_of as run
+    else:
+        raise ValueError(f"Unknown technique selected: {technique!r}")   # windows.py:156
     for p in mine:
-        process_single_video_fd(p, output_dir, **kwargs)
+        run(p, output_dir, **kwargs)
     return mine

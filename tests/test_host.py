@@ -206,3 +206,13 @@ def test_div_rn_equals_ieee_division():
         got = (t.astype(np.float64) * (1.0 / np.float64(q))).astype(np.float32)
         assert np.array_equal(want.view(np.uint32), got.view(np.uint32)), f"q={q}"
         assert np.array_equal(np.rint(want) * q, np.rint(got) * q)
+
+
+def test_process_feeds_techniques(tmp_path):
+    """feeds.process_feeds dispatches the reference GUI's two technique labels
+    (windows.py:149-156); anything else is rejected before any GPU work."""
+    from dvc_amd.feeds import process_feeds
+    with pytest.raises(ValueError):
+        process_feeds(["synthetic://64x48?frames=2"], str(tmp_path), technique="Background Subtraction")
+    with pytest.raises(TypeError):
+        process_feeds(["synthetic://64x48?frames=2"], str(tmp_path), technique="Optical Flow", min_area=3)
