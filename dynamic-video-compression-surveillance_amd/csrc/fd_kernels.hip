@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dvc_device.h"
 #include "fd_kernels.h"
@@ -784,15 +785,13 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
 }
 
 // k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
-// row, one lane per BxB block; blockIdx.z = frame of the batch.
+// row, one lane per BxB block, of frame t of the batch.
 template <int B>
-__global__ void __launch_bounds__(256) k_out(BackArgs a)
+__device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int ty, int lane, int wave)
 {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int t = blockIdx.z;
     const int W = a.g.W, H = a.g.H;
-    const int bx = blockIdx.x * 64 * B + lane * B, by = (blockIdx.y * 4 + wave) * B;
-    if (bx >= W || by >= H) return;   // no barrier below
+    const int bx = tx * 64 * B + lane * B, by = (ty * 4 + wave) * B;
+    if (bx >= W || by >= H) return;
     const uint8_t* f = a.bgr + (size_t)t * a.fstride;
     uint32_t px[B][3 * B / 4];
 #pragma unroll
@@ -900,6 +899,20 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a)
     }
 }
 
+// Grid-stride over the batch's (frame, tile) pairs with a bounded grid: a few
+// long-lived workgroups per CU keep HBM saturated while leaving wave slots to
+// the latency-bound contour-filter kernels running beside it on other streams.
+template <int B>
+__global__ void __launch_bounds__(256) k_out(BackArgs a, int ntx, int nty)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int per = ntx * nty, total = per * a.n;
+    for (int u = blockIdx.x; u < total; u += gridDim.x) {   // no barrier in the loop
+        const int t = u / per, r = u - t * per, ty = r / ntx;
+        out_tile<B>(a, t, r - ty * ntx, ty, lane, wave);
+    }
+}
+
 // --------------------------------------------------------------- launchers --
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
                         int W, int H, const GaussTaps& k, hipStream_t s)
@@ -915,9 +928,12 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
                         uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
-    // chunks: ~2560 workgroups in flight, at least 8 frames per chunk
-    int chunks = (2560 + tx * ty / 2) / (tx * ty);
-    chunks = std::max(1, std::min(chunks, n / 8));
+    // chunks: ~5120 workgroups, at least 8 frames per chunk (1080p x 63: 7 chunks
+    // of 9 frames, measured best); DVC_FRONT_WGS / DVC_FRONT_MIN override for sweeps
+    static const int target = [] { const char* e = getenv("DVC_FRONT_WGS"); return e ? std::max(1, atoi(e)) : 5120; }();
+    int chunks = (target + tx * ty / 2) / (tx * ty);
+    static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
+    chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(k_front, dim3(tx, ty, chunks), dim3(256), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
@@ -971,13 +987,18 @@ hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t m
     if (e != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     if (!a.overlay && !a.compressed) return hipSuccess;
-    if (block == 4) {
-        dim3 grid((a.g.W + 255) / 256, (a.g.H + 15) / 16, a.n);
-        hipLaunchKernelGGL(k_out<4>, grid, dim3(256), 0, s, a);
-    } else {
-        dim3 grid((a.g.W + 511) / 512, (a.g.H + 31) / 32, a.n);
-        hipLaunchKernelGGL(k_out<8>, grid, dim3(256), 0, s, a);
-    }
+    // 16 workgroups per CU (4096 on MI355X): measured best of 1k..4k beside the
+    // CCL chain; DVC_OUT_WGS overrides for sweeps
+    static const int wgs = [] {
+        if (const char* e = getenv("DVC_OUT_WGS")) return std::max(1, atoi(e));
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        return 16 * cus;
+    }();
+    const int ntx = (a.g.W + 64 * block - 1) / (64 * block), nty = (a.g.H + 4 * block - 1) / (4 * block);
+    const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
+    if (block == 4) hipLaunchKernelGGL(k_out<4>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else hipLaunchKernelGGL(k_out<8>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
     return hipGetLastError();
 }
 
