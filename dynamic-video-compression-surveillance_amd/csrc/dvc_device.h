@@ -333,10 +333,10 @@ __device__ __forceinline__ void block_dct_quant_pk(float (&X)[B * B], const DctM
     for (int i = 0; i < B; ++i)
 #pragma unroll
         for (int k = 0; k < B; k += 2) {
-            f32x2 t = (f32x2)(X[i * B]) * (f32x2){M.m[k * B], M.m[(k + 1) * B]};
+            const f32x2* mt = reinterpret_cast<const f32x2*>(M.mt + k);   // (M[k][n], M[k+1][n]) at mt[n*B/2]
+            f32x2 t = (f32x2)(X[i * B]) * mt[0];
 #pragma unroll
-            for (int n = 1; n < B; ++n)
-                t = __builtin_elementwise_fma((f32x2)(X[i * B + n]), (f32x2){M.m[k * B + n], M.m[(k + 1) * B + n]}, t);
+            for (int n = 1; n < B; ++n) t = __builtin_elementwise_fma((f32x2)(X[i * B + n]), mt[n * B / 2], t);
             T[i * B + k] = t.x;
             T[i * B + k + 1] = t.y;
         }
@@ -355,10 +355,10 @@ __device__ __forceinline__ void block_dct_quant_pk(float (&X)[B * B], const DctM
     for (int k = 0; k < B; ++k)
 #pragma unroll
         for (int n = 0; n < B; n += 2) {
-            f32x2 t = (f32x2)(X[k * B]) * (f32x2){M.m[n], M.m[n + 1]};
+            const f32x2* mp = reinterpret_cast<const f32x2*>(M.m + n);    // (M[l][n], M[l][n+1]) at mp[l*B/2]
+            f32x2 t = (f32x2)(X[k * B]) * mp[0];
 #pragma unroll
-            for (int l = 1; l < B; ++l)
-                t = __builtin_elementwise_fma((f32x2)(X[k * B + l]), (f32x2){M.m[l * B + n], M.m[l * B + n + 1]}, t);
+            for (int l = 1; l < B; ++l) t = __builtin_elementwise_fma((f32x2)(X[k * B + l]), mp[l * B / 2], t);
             T[k * B + n] = t.x;
             T[k * B + n + 1] = t.y;
         }

@@ -25,8 +25,10 @@ struct GaussTaps {
     uint16_t t[64];
 };
 
-struct DctMat {
-    float m[64];  // BxB row-major orthonormal DCT-II basis M[k][n], float32
+struct alignas(8) DctMat {
+    float m[64];   // BxB row-major orthonormal DCT-II basis M[k][n], float32
+    float mt[64];  // its transpose: the pairs (M[k][n], M[k+1][n]) adjacent for
+                   // 64-bit scalar kernarg loads (block_dct_quant_pk)
 };
 
 // Device buffers of the contour-filter stage: frame f of a batch owns the f-th

@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "fd_kernels.h"
+
 namespace dvc_host {
 
 // Set the calling thread's dvc_last_error() text; returns `code`.
@@ -11,7 +13,7 @@ const char* last_error();
 // getGaussianKernelBitExact values in double (n odd <= 63).
 void gauss_f64(int n, double sigma, double* k);
 // BxB orthonormal DCT-II basis M[k][n], float32.
-void dct_matrix(int B, float* M);
+void dct_matrix(int B, dvc::DctMat& M);   // M and its transpose
 
 }  // namespace dvc_host
 

@@ -207,7 +207,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     g.up = (float)(1. / p.pyr_scale);
     g.flow_thr = p.flow_threshold;
     poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
-    dvc_host::dct_matrix(8, h->M.m);
+    dvc_host::dct_matrix(8, h->M);
 
     auto bad = [&](hipError_t e, const char* what) {
         int rc = fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "%s: %s", what, hipGetErrorString(e));
@@ -600,7 +600,7 @@ int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int w
         o.ostride = 3 * N;
         o.quant = quant;
         o.qinv = 1.0 / (double)quant;
-        dvc_host::dct_matrix(8, o.M.m);
+        dvc_host::dct_matrix(8, o.M);
         e = dvc::of_launch_out(g, b, o, 1, nullptr);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();

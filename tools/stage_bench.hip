@@ -98,7 +98,7 @@ int main(int argc, char** argv)
     a.acc0_fixed = 1;
     for (int k = 0; k < 4; ++k)
         for (int j = 0; j < 4; ++j)
-            a.M.m[k * 4 + j] = (float)((k == 0 ? std::sqrt(0.25) : std::sqrt(0.5)) * std::cos(M_PI * (2 * j + 1) * k / 8.0));
+            a.M.m[k * 4 + j] = a.M.mt[j * 4 + k] = (float)((k == 0 ? std::sqrt(0.25) : std::sqrt(0.5)) * std::cos(M_PI * (2 * j + 1) * k / 8.0));
     a.stats = stats;
     double tf = 0, tc = 0, tb = 0;
     for (int r = 0; r < reps; ++r) {
