@@ -987,13 +987,13 @@ hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t m
     if (e != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     if (!a.overlay && !a.compressed) return hipSuccess;
-    // 16 workgroups per CU (4096 on MI355X): measured best of 1k..4k beside the
-    // CCL chain; DVC_OUT_WGS overrides for sweeps
+    // 64 workgroups per CU (16384 on MI355X, ~2 tiles each at 1080p x 63):
+    // measured best of 2k..34k beside the CCL chain; DVC_OUT_WGS overrides
     static const int wgs = [] {
         if (const char* e = getenv("DVC_OUT_WGS")) return std::max(1, atoi(e));
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        return 16 * cus;
+        return 64 * cus;
     }();
     const int ntx = (a.g.W + 64 * block - 1) / (64 * block), nty = (a.g.H + 4 * block - 1) / (4 * block);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
