@@ -216,3 +216,55 @@ def test_process_feeds_techniques(tmp_path):
         process_feeds(["synthetic://64x48?frames=2"], str(tmp_path), technique="Background Subtraction")
     with pytest.raises(TypeError):
         process_feeds(["synthetic://64x48?frames=2"], str(tmp_path), technique="Optical Flow", min_area=3)
+
+
+def _write_stream(path, n, fps, shape=(8, 16, 3), val=7):
+    from dvc_amd import video_io
+    w = video_io.open_sink(str(path), fps, (shape[1], shape[0]), is_color=len(shape) == 3)
+    for _ in range(n):
+        w.write(np.full(shape, val, np.uint8))
+    w.release()
+
+
+def test_performance_report(tmp_path, capsys):
+    """performance_analysis.py:152-249 restated: CSV columns, durations, sizes, reduction."""
+    import csv
+    from dvc_amd import performance_analysis as pa
+    from dvc_amd.frame_differencing import write_execution_times as fd_times
+    from dvc_amd.motion_compression_opt import write_execution_times as of_times
+    fd = tmp_path / "clipA"
+    fd.mkdir()
+    fd_times(fd / "execution_times.txt", 59, 3.0, 3.0 / 59)
+    _write_stream(fd / "dilated_motion_mask_video.mp4", 60, 30)
+    _write_stream(fd / "compressed_final_video.mp4", 30, 30)      # half the bytes
+    of = tmp_path / "clipB"
+    of.mkdir()
+    of_times(of / "execution_times.txt", (99, 2.0, 0.0202), (99, 1.0, 0.0101))
+    _write_stream(of / "overlay.mp4", 100, 25)
+    _write_stream(of / "compressed.mp4", 100, 25)
+    (tmp_path / "junk").mkdir()
+    (tmp_path / "junk" / "execution_times.txt").write_text("nonsense\n")
+    pa.main(["pa", str(tmp_path)])
+    out = capsys.readouterr().out
+    assert "Error parsing" in out and "CSV saved in" in out
+    rows = list(csv.DictReader(open(tmp_path / "performance" / "performance_data.csv")))
+    assert list(rows[0].keys()) == pa.FIELDNAMES
+    a, b = rows
+    assert a["video"] == "clipA" and int(a["md_frames"]) == 59 and int(a["cp_frames"]) == 0
+    assert float(a["video_duration_seconds"]) == 2.0
+    assert float(a["conversion_time_per_minute (s/min)"]) == 90.0
+    hdr = 256   # NpyStreamWriter header
+    assert int(a["original_size_bytes"]) == hdr + 60 * 8 * 16 * 3
+    assert float(a["reduction_percentage (%)"]) == pytest.approx(100 * 30 * 384 / (hdr + 60 * 384))
+    assert b["video"] == "clipB" and int(b["cp_frames"]) == 99
+    assert float(b["total_processing_time (s)"]) == 3.0 and float(b["video_duration_seconds"]) == 4.0
+
+
+def test_performance_report_parse_rules(tmp_path):
+    from dvc_amd.performance_analysis import parse_execution_times
+    p = tmp_path / "e.txt"
+    p.write_text("Motion Detection:\nFrames processed: 5\nTotal time: 1.5 seconds\nAverage time per frame: 0.3 seconds\n")
+    d = parse_execution_times(p)   # no Compression section, no total line: total = md + cp
+    assert (d["cp_frames"], d["cp_time"], d["total_processing_time"]) == (0, 0, 1.5)
+    p.write_text("")
+    assert parse_execution_times(p) is None
