@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/dvc.h"
@@ -105,21 +106,29 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 
 }  // namespace
 
-// Contour-filter scratch of one batch in flight (max_batch frames).
+// Buffers of one batch in flight (max_batch frames): motion masks, contour-
+// filter scratch, kept masks and the dilate -> accumulate -> out bit fields.
 struct Slot {
     dvc::CclBufs c{};
     uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;   // k_dilate -> k_acc -> k_out bits
-    hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_back = nullptr;
+    hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_acc = nullptr, ev_out = nullptr;
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
 };
+
+// Batches in flight: three slots; the contour filter has no recurrence across
+// batches, so consecutive batches may alternate between up to two streams.
+constexpr int NSLOT = 3, NCCL_MAX = 2;
 
 struct dvc_fd {
     dvc_fd_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;  // front + contour filter (and prime); the caller's stream if given
+    hipStream_t stream = nullptr;  // prime + completion join; the caller's stream if given
     bool own_stream = false;
-    hipStream_t s_front = nullptr; // blur/threshold front (previous gray), internal
-    hipStream_t s_back = nullptr;  // back chain (accumulated mask), internal
+    hipStream_t s_front = nullptr;       // blur/threshold front (previous-gray recurrence)
+    hipStream_t s_ccl[NCCL_MAX] = {};    // contour filter of batch i on s_ccl[i % nccl]
+    int nccl = 1;
+    hipStream_t s_acc = nullptr;         // dilate + accumulate (accumulated-mask recurrence)
+    hipStream_t s_out = nullptr;         // overlay + compressed frames
     dvc::RowGeom g{};
     dvc::GaussTaps kprime{};
     dvc::DctMat M{};
@@ -129,8 +138,7 @@ struct dvc_fd {
     size_t sstride = 0;  // static-block bit words per frame
     uint64_t frames = 0, seq = 0;  // frames stepped, batches launched
     int last_n = 0;                // frames of the last batch
-    // Two slots: the front + contour filter of batch i+1 overlap the back of batch i.
-    Slot slot[2];
+    Slot slot[NSLOT];
     // device state
     uint8_t* gray[2] = {nullptr, nullptr};  // previous blurred gray (fd:77, 133): gray[gcur]
     int gcur = 0;
@@ -154,7 +162,7 @@ static void free_all(dvc_fd* h)
                        s.dblk, s.rblk, s.sbits};
         for (void* p : dev)
             if (p) (void)hipFree(p);
-        for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_back})
+        for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_acc, s.ev_out})
             if (e) (void)hipEventDestroy(e);
     }
     void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
@@ -164,8 +172,8 @@ static void free_all(dvc_fd* h)
     for (void* p : pin)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-    if (h->s_back) (void)hipStreamDestroy(h->s_back);
-    if (h->s_front) (void)hipStreamDestroy(h->s_front);
+    for (hipStream_t st : {h->s_front, h->s_ccl[0], h->s_ccl[1], h->s_acc, h->s_out})
+        if (st) (void)hipStreamDestroy(st);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
 }
 
@@ -178,8 +186,8 @@ static hipError_t dalloc(T** p, size_t bytes)
 static hipError_t sync_all(dvc_fd* h)
 {
     hipError_t e = hipStreamSynchronize(h->stream);
-    if (e == hipSuccess && h->s_front) e = hipStreamSynchronize(h->s_front);
-    if (e == hipSuccess && h->s_back) e = hipStreamSynchronize(h->s_back);
+    for (hipStream_t st : {h->s_front, h->s_ccl[0], h->s_ccl[1], h->s_acc, h->s_out})
+        if (e == hipSuccess && st) e = hipStreamSynchronize(st);
     return e;
 }
 
@@ -243,17 +251,22 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bad(e, "hipSetDevice");
     if (hip_stream) h->stream = (hipStream_t)hip_stream;
-    // priorities: the contour filter (latency-bound, the critical chain under
-    // concurrency) high, the VALU-bound front low; measured +1% at 1080p
+    // priorities: the latency-bound contour filter and accumulate chains high,
+    // the VALU-bound front low
     int plo = 0, phi = 0;
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
     auto mk = [](hipStream_t* st, int prio) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio); };
     if (!hip_stream) {
-        if ((e = mk(&h->stream, phi)) != hipSuccess) return bad(e, "hipStreamCreate");
+        if ((e = mk(&h->stream, 0)) != hipSuccess) return bad(e, "hipStreamCreate");
         h->own_stream = true;
     }
-    if ((e = mk(&h->s_back, 0)) != hipSuccess) return bad(e, "hipStreamCreate");
-    if ((e = mk(&h->s_front, plo)) != hipSuccess) return bad(e, "hipStreamCreate");
+    // four internal streams fit the default 4 hardware queues (GPU_MAX_HW_QUEUES);
+    // DVC_CCL_STREAMS=2 adds a second contour-filter stream
+    if (const char* ev = getenv("DVC_CCL_STREAMS")) h->nccl = std::max(1, std::min(NCCL_MAX, atoi(ev)));
+    for (int i = 0; i < h->nccl; ++i)
+        if ((e = mk(&h->s_ccl[i], phi)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (auto sp : {std::make_pair(&h->s_front, plo), std::make_pair(&h->s_acc, phi), std::make_pair(&h->s_out, 0)})
+        if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     for (Slot& s : h->slot) {
         size_t sz[10];
@@ -267,7 +280,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if ((e = dalloc(&s.dblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = dalloc(&s.rblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
-        for (hipEvent_t* ev : {&s.ev_front, &s.ev_ccl, &s.ev_back})
+        for (hipEvent_t* ev : {&s.ev_front, &s.ev_ccl, &s.ev_acc, &s.ev_out})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
     struct { void** ptr; size_t bytes; } allocs[] = {
@@ -335,26 +348,31 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 
 }  // extern "C"
 
-// Enqueue one batch of n <= max_batch device-resident frames:
-//   s_front: [wait ccl(i-2)] front(i) -> ev_front          (previous gray in order)
-//   stream:  [wait ev_front, back(i-2)] contour filter(i) -> ev_ccl
-//   s_back:  [wait ev_ccl] back(i) -> ev_back              (accumulated mask in order)
-// so front(i+2), the contour filter of batch i+1 and the back of batch i run
-// concurrently: VALU-bound, latency-bound and HBM-bound work side by side.
+// Enqueue one batch i of n <= max_batch device-resident frames, slot S = i % 3
+// (j = i - 3 = the slot's previous batch):
+//   s_front:         [wait ccl(j)]            front(i) -> ev_front   (S.mbits free)
+//   s_ccl[i % 2]:    [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
+//   s_acc:           [wait ev_ccl, out(j)]    dilate + accumulate(i) -> ev_acc (S bits free)
+//   s_out:           [wait ev_acc]            k_out(i) -> ev_out
+// so front(i+2), the contour filters of i+1 and i, the accumulation of i and
+// the output of i-1 can all be in flight; only the two recurrences (previous
+// gray, accumulated mask) are serial, each on its own stream.
 static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride)
 {
-    Slot& S = h->slot[h->seq & 1];
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));   // S.mbits free
+    Slot& S = h->slot[h->seq % NSLOT];
+    hipStream_t s_ccl = h->s_ccl[h->seq % h->nccl];
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
     HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], S.c.mbits, h->g,
                              h->p.ithresh, h->s_front));
     HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
-    HIP_OK(hipStreamWaitEvent(h->stream, S.ev_front, 0));
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->stream, S.ev_back, 0));    // S.kbits free
-    HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, h->stream));
-    HIP_OK(hipEventRecord(S.ev_ccl, h->stream));
-    HIP_OK(hipStreamWaitEvent(h->s_back, S.ev_ccl, 0));
+    HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_front, 0));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_acc, 0));
+    HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, s_ccl));
+    HIP_OK(hipEventRecord(S.ev_ccl, s_ccl));
+    HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_ccl, 0));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_out, 0));
     dvc::BackArgs a{};
     a.g = h->g;
     a.bgr = d;
@@ -386,7 +404,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.M = h->M;
     a.stats = h->stats;
     a.dbg_dil = h->dbg_dil;
-    // KTIMING: events around k_out (the HBM-bound kernel): k_acc | ev | k_out | ev
+    // KTIMING: events around k_out (the HBM-bound kernel) on s_out
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
     if (timed) {
         while (h->ev.size() < h->ev_used + 2) {
@@ -395,12 +413,16 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::launch_back(a, h->p.block, h->s_back, timed ? h->ev[h->ev_used] : nullptr));
+    HIP_OK(dvc::launch_accumulate(a, h->p.block, h->s_acc));
+    HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
+    HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
+    if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
+    HIP_OK(dvc::launch_out(a, h->p.block, h->s_out));
     if (timed) {
-        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_back));
+        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
         h->ev_used += 2;
     }
-    HIP_OK(hipEventRecord(S.ev_back, h->s_back));
+    HIP_OK(hipEventRecord(S.ev_out, h->s_out));
     S.recorded = true;
     h->seq++;
     h->frames += (uint64_t)n;
@@ -440,8 +462,8 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
         HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_front));
         int rc = enqueue_batch(h, h->d_in, (int)row, 3 * N, m, ov ? h->d_ov : nullptr, cp ? h->d_cp : nullptr, 3 * N);
         if (rc) return rc;
-        if (ov) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_back));
-        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_back));
+        if (ov) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_out));
+        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_out));
         HIP_OK(sync_all(h));
         for (int t = 0; t < m; ++t) {
             if (ov) std::memcpy(ov + (size_t)t * ostride, h->h_ov + (size_t)t * 3 * N, 3 * N);
@@ -450,10 +472,10 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
     }
     if (acc_out) {
         if (devp) {
-            HIP_OK(hipMemcpyAsync(acc_out, h->acc, N, hipMemcpyDeviceToDevice, h->s_back));
+            HIP_OK(hipMemcpyAsync(acc_out, h->acc, N, hipMemcpyDeviceToDevice, h->s_acc));
         } else {
-            HIP_OK(hipMemcpyAsync(h->h_acc, h->acc, N, hipMemcpyDeviceToHost, h->s_back));
-            HIP_OK(hipStreamSynchronize(h->s_back));
+            HIP_OK(hipMemcpyAsync(h->h_acc, h->acc, N, hipMemcpyDeviceToHost, h->s_acc));
+            HIP_OK(hipStreamSynchronize(h->s_acc));
             std::memcpy(acc_out, h->h_acc, N);
         }
     }
@@ -509,7 +531,7 @@ int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* dst)
         return DVC_OK;
     }
     // the last frame of the last batch
-    const dvc::CclBufs c = h->slot[(h->seq - 1) & 1].c.frame((size_t)h->last_n - 1, h->g);
+    const dvc::CclBufs c = h->slot[(h->seq - 1) % NSLOT].c.frame((size_t)h->last_n - 1, h->g);
     const uint64_t* src = plane == DVC_PLANE_MOTION ? c.mbits
                         : plane == DVC_PLANE_FILTERED ? c.kbits
                         : plane == DVC_PLANE_DILATED ? h->dbg_dil : nullptr;

@@ -95,7 +95,9 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
                         uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
 int band_rows(const RowGeom& g);
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
-// k_dilate, k_acc, then k_out; `mid` (nullable) is recorded before k_out
-hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t mid);
+// k_dilate then k_acc (the accumulated-mask recurrence: batches in order)
+hipError_t launch_accumulate(const BackArgs& a, int block, hipStream_t s);
+// k_out (overlay + compressed frames; no recurrence, nothing if both are NULL)
+hipError_t launch_out(const BackArgs& a, int block, hipStream_t s);
 
 }  // namespace dvc

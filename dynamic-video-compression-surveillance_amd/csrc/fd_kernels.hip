@@ -981,11 +981,13 @@ static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_back(const BackArgs& a, int block, hipStream_t s, hipEvent_t mid)
+hipError_t launch_accumulate(const BackArgs& a, int block, hipStream_t s)
 {
-    hipError_t e = block == 4 ? launch_acc<4>(a, s) : launch_acc<8>(a, s);
-    if (e != hipSuccess) return e;
-    if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
+    return block == 4 ? launch_acc<4>(a, s) : launch_acc<8>(a, s);
+}
+
+hipError_t launch_out(const BackArgs& a, int block, hipStream_t s)
+{
     if (!a.overlay && !a.compressed) return hipSuccess;
     // 64 workgroups per CU (16384 on MI355X, ~2 tiles each at 1080p x 63):
     // measured best of 2k..34k beside the CCL chain; DVC_OUT_WGS overrides

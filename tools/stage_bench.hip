@@ -113,7 +113,8 @@ int main(int argc, char** argv)
         CK(dvc::launch_ccl(c, g, n, 1000, nullptr));
         CK(hipDeviceSynchronize());
         auto t2 = std::chrono::steady_clock::now();
-        CK(dvc::launch_back(a, 4, nullptr, nullptr));
+        CK(dvc::launch_accumulate(a, 4, nullptr));
+        CK(dvc::launch_out(a, 4, nullptr));
         CK(hipDeviceSynchronize());
         auto t3 = std::chrono::steady_clock::now();
         if (r > 0) {
