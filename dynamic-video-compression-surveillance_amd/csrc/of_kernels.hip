@@ -244,6 +244,11 @@ struct FlowArgs {
     int n;
 };
 
+// MB > 0: box radius m known at compile time (the reference's winsize 9 -> 4):
+// the vertical sums run one thread per (column, channel), the column's M values
+// converted to double once in registers; MB = 0: any m, one thread per
+// (row, column) re-reading M per tap.
+template <int MB>
 __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) double lds_d[];
@@ -367,39 +372,63 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     }
     __syncthreads();
 
-    // ---- vertical box sums (double, rows in order), into registers, then
-    // aliased over sM: FL_H x RW x 5 doubles
-    constexpr int VMAX = (FL_H * (FL_W + 2 * OF_MAX_BOX_M) + 255) / 256;
-    double vs[VMAX][5];
-    const int nv = FL_H * RW;
-#pragma unroll
-    for (int q = 0; q < VMAX; ++q) {
-        const int idx = tid + 256 * q;
-        if (idx >= nv) break;
-        const int i = idx / RW, j = idx - i * RW;
-        const int y = y0 + i, x = x0 - m + j;
-#pragma unroll
-        for (int c = 0; c < 5; ++c) vs[q][c] = 0.0;
-        if (y >= h || x < 0 || x >= w) continue;
-        double s[5] = {0, 0, 0, 0, 0};
-        for (int jj = -m; jj <= m; ++jj) {
-            const float* M = sM + (size_t)((min(max(y + jj, 0), h - 1) - (y0 - m)) * RW + j) * 5;
-#pragma unroll
-            for (int c = 0; c < 5; ++c) s[c] += (double)M[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 5; ++c) vs[q][c] = s[c];
-    }
-    __syncthreads();
+    // ---- vertical box sums (double, rows in order) into sV, aliased over sM:
+    // FL_H x RW x 5 doubles
     double* sV = lds_d;
+    if constexpr (MB > 0) {
+        constexpr int CR = FL_H + 2 * MB;   // M rows of a column
+        const int j = tid / 5, c = tid - 5 * j;
+        const int x = x0 - m + j;
+        const bool colv = j < RW && x >= 0 && x < w;
+        double col[CR];
 #pragma unroll
-    for (int q = 0; q < VMAX; ++q) {
-        const int idx = tid + 256 * q;
-        if (idx >= nv) break;
+        for (int r = 0; r < CR; ++r) {   // rows clamped into the image (replicated border)
+            const int yy = min(max(y0 - m + r, 0), h - 1) - (y0 - m);
+            col[r] = colv ? (double)sM[(size_t)(yy * RW + j) * 5 + c] : 0.0;
+        }
+        __syncthreads();
+        if (colv) {
 #pragma unroll
-        for (int c = 0; c < 5; ++c) sV[(size_t)idx * 5 + c] = vs[q][c];
+            for (int i = 0; i < FL_H; ++i) {
+                double sum = 0.0;
+#pragma unroll
+                for (int jj = 0; jj <= 2 * MB; ++jj) sum += col[i + jj];
+                sV[(size_t)(i * RW + j) * 5 + c] = sum;
+            }
+        }
+        __syncthreads();
+    } else {
+        constexpr int VMAX = (FL_H * (FL_W + 2 * OF_MAX_BOX_M) + 255) / 256;
+        double vs[VMAX][5];
+        const int nv = FL_H * RW;
+#pragma unroll
+        for (int q = 0; q < VMAX; ++q) {
+            const int idx = tid + 256 * q;
+            if (idx >= nv) break;
+            const int i = idx / RW, j = idx - i * RW;
+            const int y = y0 + i, x = x0 - m + j;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) vs[q][c] = 0.0;
+            if (y >= h || x < 0 || x >= w) continue;
+            double s[5] = {0, 0, 0, 0, 0};
+            for (int jj = -m; jj <= m; ++jj) {
+                const float* M = sM + (size_t)((min(max(y + jj, 0), h - 1) - (y0 - m)) * RW + j) * 5;
+#pragma unroll
+                for (int c = 0; c < 5; ++c) s[c] += (double)M[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 5; ++c) vs[q][c] = s[c];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < VMAX; ++q) {
+            const int idx = tid + 256 * q;
+            if (idx >= nv) break;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) sV[(size_t)idx * 5 + c] = vs[q][c];
+        }
+        __syncthreads();
     }
-    __syncthreads();
 
     // ---- horizontal box sums, flow = G^-1 h (oc_update_flow_box); a wave covers
     // two 32-px rows (lanes 0-31 row i, 32-63 row i+1)
@@ -879,7 +908,8 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.dst = A.last ? nullptr : L.flow[it & 1];
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
-            hipLaunchKernelGGL(k_flow, grid, dim3(256), lds, s, A);
+            if (g.m == 4) hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
+            else hipLaunchKernelGGL(k_flow<0>, grid, dim3(256), lds, s, A);
         }
     }
     return hipGetLastError();
