@@ -244,18 +244,22 @@ struct FlowArgs {
     int n;
 };
 
-// MB > 0: box radius m known at compile time (the reference's winsize 9 -> 4):
-// the vertical sums run one thread per (column, channel), the column's M values
-// converted to double once in registers; MB = 0: any m, one thread per
-// (row, column) re-reading M per tap.
-template <int MB>
-__global__ void __launch_bounds__(256) k_flow(FlowArgs A)
+// One tile of k_flow. MB > 0: box radius m known at compile time (the
+// reference's winsize 9 -> 4): constant tile geometry, the vertical sums one
+// thread per (column, channel) with the column's M converted to double once in
+// registers. INT: an interior tile — tile + box halo inside the image and at
+// least 5 px from its edges — so no coordinate is clamped, no position skipped
+// and no border weight applied (the same arithmetic on the same values as the
+// general form). MB = 0: any m, clamped everywhere, one thread per (row,
+// column) re-reading M per tap.
+template <int MB, bool INT>
+__device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
 {
-    extern __shared__ __attribute__((aligned(16))) double lds_d[];
     float* sM = reinterpret_cast<float*>(lds_d);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, t = blockIdx.z;
     const OfGeom& g = A.g;
-    const int w = A.lv.w, h = A.lv.h, m = g.m;
+    const int w = A.lv.w, h = A.lv.h;
+    const int m = MB > 0 ? MB : g.m;
     const int RW = FL_W + 2 * m, RH = FL_H + 2 * m;
     const int x0 = blockIdx.x * FL_W, y0 = blockIdx.y * FL_H;
     const size_t lvpx = (size_t)w * h;
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     // image and every load unconditional (results of out-of-image positions
     // are discarded), so a group's flow / R0 loads and then its bilinear R1
     // gathers are all in flight together instead of one dependent round trip
-    // pair per position.
+    // pair per position. Pixel offsets are 32-bit (a level plane < 2^31 floats).
     constexpr int MQ = 2;
     const int npos = RH * RW;
     for (int q0 = tid; q0 < npos; q0 += 256 * MQ) {
@@ -282,19 +286,26 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
             idx[u] = q0 + 256 * u;
             const int i = idx[u] / RW, j = idx[u] - i * RW;
             const int y = y0 - m + i, x = x0 - m + j;
-            ok[u] = idx[u] < npos && y >= 0 && y < h && x >= 0 && x < w;
-            ys[u] = min(max(y, 0), h - 1);
-            xs[u] = min(max(x, 0), w - 1);
+            if constexpr (INT) {
+                ok[u] = idx[u] < npos;
+                ys[u] = ok[u] ? y : y0;
+                xs[u] = x;
+            } else {
+                ok[u] = idx[u] < npos && y >= 0 && y < h && x >= 0 && x < w;
+                ys[u] = min(max(y, 0), h - 1);
+                xs[u] = min(max(x, 0), w - 1);
+            }
+            const uint32_t pix = (uint32_t)(ys[u] * w + xs[u]);
             dxv[u] = 0.f;
             dyv[u] = 0.f;
             if (A.src_mode == 2) {   // uniform
-                const float2 f = *reinterpret_cast<const float2*>(src + ((size_t)ys[u] * w + xs[u]) * 2);
+                const float2 f = *reinterpret_cast<const float2*>(src + 2u * pix);
                 dxv[u] = f.x;
                 dyv[u] = f.y;
             } else if (A.src_mode == 1) {
                 const LinTap ty = A.lv.uy[ys[u]], tx = A.lv.ux[xs[u]];
-                const float* ra = src + (size_t)ty.s0 * A.sw * 2;
-                const float* rb = src + (size_t)ty.s1 * A.sw * 2;
+                const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
+                const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
                 float v[2];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
@@ -305,7 +316,7 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
                 dxv[u] = v[0] * g.up;
                 dyv[u] = v[1] * g.up;
             }
-            const float* r0 = R0 + ((size_t)ys[u] * w + xs[u]) * 5;
+            const float* r0 = R0 + 5u * pix;
 #pragma unroll
             for (int c = 0; c < 5; ++c) r0v[u][c] = r0[c];
         }
@@ -320,8 +331,8 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
             fyv[u] = fy - (float)y1;
             inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
             const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
-            const float* p = R1 + ((size_t)y1c * w + x1c) * 5;
-            const float* q = p + (size_t)w * 5;
+            const float* p = R1 + 5u * (uint32_t)(y1c * w + x1c);
+            const float* q = p + 5u * (uint32_t)w;
 #pragma unroll
             for (int c = 0; c < 10; ++c) {
                 pq[u][c] = p[c];
@@ -357,10 +368,12 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
             r3 = (r0[1] - r3) * 0.5f;
             r2 += r4 * dy + r6 * dx;
             r3 += r6 * dy + r5 * dx;
-            if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
-                const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
-                                    (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
-                r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+            if constexpr (!INT) {
+                if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
+                    const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
+                                        (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+                    r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+                }
             }
             float* M = sM + (size_t)idx[u] * 5;
             M[0] = r4 * r4 + r6 * r6;
@@ -379,12 +392,12 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
         constexpr int CR = FL_H + 2 * MB;   // M rows of a column
         const int j = tid / 5, c = tid - 5 * j;
         const int x = x0 - m + j;
-        const bool colv = j < RW && x >= 0 && x < w;
+        const bool colv = INT ? j < RW : (j < RW && x >= 0 && x < w);
         double col[CR];
 #pragma unroll
         for (int r = 0; r < CR; ++r) {   // rows clamped into the image (replicated border)
-            const int yy = min(max(y0 - m + r, 0), h - 1) - (y0 - m);
-            col[r] = colv ? (double)sM[(size_t)(yy * RW + j) * 5 + c] : 0.0;
+            const int yy = INT ? r : min(max(y0 - m + r, 0), h - 1) - (y0 - m);
+            col[r] = colv ? (double)sM[(yy * RW + j) * 5 + c] : 0.0;
         }
         __syncthreads();
         if (colv) {
@@ -393,7 +406,7 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
                 double sum = 0.0;
 #pragma unroll
                 for (int jj = 0; jj <= 2 * MB; ++jj) sum += col[i + jj];
-                sV[(size_t)(i * RW + j) * 5 + c] = sum;
+                sV[(i * RW + j) * 5 + c] = sum;
             }
         }
         __syncthreads();
@@ -433,18 +446,27 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     // ---- horizontal box sums, flow = G^-1 h (oc_update_flow_box); a wave covers
     // two 32-px rows (lanes 0-31 row i, 32-63 row i+1)
     float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
-    unsigned long long nmot = 0;
     for (int i2 = wave; i2 < FL_H / 2; i2 += 4) {
         const int i = 2 * i2 + (lane >> 5);
         const int y = y0 + i, x = x0 + (lane & 31);
-        const bool act = y < h && x < w;
+        const bool act = INT || (y < h && x < w);
         float fxo = 0.f, fyo = 0.f;
         if (act) {
             double hs[5] = {0, 0, 0, 0, 0};
-            for (int ii = -m; ii <= m; ++ii) {
-                const double* v = sV + (size_t)(i * RW + (min(max(x + ii, 0), w - 1) - (x0 - m))) * 5;
+            if constexpr (MB > 0) {
 #pragma unroll
-                for (int c = 0; c < 5; ++c) hs[c] += v[c];
+                for (int ii = -MB; ii <= MB; ++ii) {
+                    const int xx = INT ? (lane & 31) + MB + ii : min(max(x + ii, 0), w - 1) - (x0 - m);
+                    const double* v = sV + (i * RW + xx) * 5;
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) hs[c] += v[c];
+                }
+            } else {
+                for (int ii = -m; ii <= m; ++ii) {
+                    const double* v = sV + (size_t)(i * RW + (min(max(x + ii, 0), w - 1) - (x0 - m))) * 5;
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) hs[c] += v[c];
+                }
             }
             const double g11 = hs[0] * g.box_scale, g12 = hs[1] * g.box_scale, g22 = hs[2] * g.box_scale;
             const double h1 = hs[3] * g.box_scale, h2 = hs[4] * g.box_scale;
@@ -453,7 +475,7 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
             fyo = (float)((g22 * h1 - g12 * h2) * idet);
         }
         if (!A.last) {
-            if (act) *reinterpret_cast<float2*>(dst + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
+            if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fxo, fyo);
         } else {
             // of:82-83: cartToPolar magnitude (float) > flow_threshold
             const float mag = sqrtf(fxo * fxo + fyo * fyo);
@@ -465,12 +487,25 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
                 mr[((size_t)y * g.WW + (x0 >> 6)) * 2 + half] = (uint32_t)(word >> (lane & 32));
                 if (half == 0 && x0 + 32 >= w) mr[((size_t)y * g.WW + (x0 >> 6)) * 2 + 1] = 0u;   // no tile owns it
             }
-            nmot += (unsigned long long)__popcll(word);
             if (A.dbg_flow && t == A.n - 1 && act)
                 *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
         }
     }
-    (void)nmot;
+}
+
+template <int MB>
+__global__ void __launch_bounds__(256) k_flow(FlowArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_d[];
+    if constexpr (MB > 0) {
+        const int x0 = blockIdx.x * FL_W, y0 = blockIdx.y * FL_H;
+        const bool interior = x0 - MB >= 5 && x0 + FL_W + MB <= A.lv.w - 5 && y0 - MB >= 5 &&
+                              y0 + FL_H + MB <= A.lv.h - 5;   // uniform
+        if (interior) flow_tile<MB, true>(A, lds_d);
+        else flow_tile<MB, false>(A, lds_d);
+    } else {
+        flow_tile<0, false>(A, lds_d);
+    }
 }
 
 // -------------------------------------------------------------------- vote --
