@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <numeric>
 
 #include "dvc_device.h"
 #include "of_kernels.h"
@@ -41,7 +42,14 @@ namespace {
 constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
 constexpr int FL_W = 32, FL_H = 16;   // flow tile (32 wide: <= 26 KB LDS, 6 workgroups per CU)
 
-__device__ __forceinline__ long long ring(long long a, int n) { return ((a % n) + n) % n; }
+// Ring slot of frame number a. The launchers pass frame numbers through
+// reduce_frame(), which keeps them below 2^31, so the modulo is 32-bit (a 64-bit
+// one is a long VALU + SALU expansion per workgroup).
+__device__ __forceinline__ int ring(long long a, int n)
+{
+    const int r = (int)a % n;
+    return r < 0 ? r + n : r;
+}
 
 // ------------------------------------------------- polynomial expansion -----
 // Steps C and D of FarnebackPolyExp (oc_poly_exp) for one tile whose smoothed
@@ -894,9 +902,21 @@ static int of_band_rows(const OfGeom& g, size_t* lds)
     }
 }
 
+// Frame numbers as the kernels see them: a0 itself up to RED_K (so the vote's
+// `a - window >= 1` and `min(a, window)` read the true values; window <= 127),
+// beyond it RED_K + (a0 - RED_K) mod lcm(RS, RB) — the same slot in both rings.
+static constexpr long long RED_K = 256;
+static long long reduce_frame(const OfGeom& g, long long a0)
+{
+    if (a0 <= RED_K) return a0;
+    const long long p = std::lcm((long long)g.RS, (long long)g.RB);
+    return RED_K + (a0 - RED_K) % p;
+}
+
 hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
                              size_t fstride, long long a0, int n, hipStream_t s)
 {
+    a0 = reduce_frame(g, a0);
     if (n <= 0) return hipSuccess;
     {
         dim3 grid((g.W + PT_W - 1) / PT_W, (g.H + PT_H - 1) / PT_H, n);
@@ -916,6 +936,7 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
                           hipStream_t s)
 {
+    a0 = reduce_frame(g, a0);
     const size_t lds = std::max((size_t)(FL_H + 2 * g.m) * (FL_W + 2 * g.m) * 5 * 4,
                                 (size_t)FL_H * (FL_W + 2 * g.m) * 5 * 8);
     for (int k = k_hi; k >= k_lo; --k) {
@@ -952,6 +973,7 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
 
 hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s)
 {
+    a0 = reduce_frame(g, a0);
     const size_t nchunk = (size_t)g.H * g.WW * 4;
     hipLaunchKernelGGL(k_vote, dim3((unsigned)((nchunk + 255) / 256)), dim3(256), 0, s, g, b, a0, window, n);
     size_t lds = 0;

@@ -114,6 +114,16 @@ def test_of_parity_window_eviction(gpu_lib, oracle_lib):
     _run_pair(gpu_lib, oracle_lib, clip(320, 176, 9, seed=4, n_objects=4), window_size=3, alpha_fraction=0.4)
 
 
+def test_of_parity_long_run(gpu_lib, oracle_lib):
+    """> 256 frames: the launchers reduce frame numbers modulo the ring periods
+    (reduce_frame in of_kernels.hip); slots, the vote window and its eviction
+    must carry on exactly, batched and per frame."""
+    from dvc_amd.synthetic import clip
+    frames = clip(64, 48, 301, seed=3, n_objects=2)
+    _run_pair(gpu_lib, oracle_lib, frames, batch=16, window_size=7)
+    _run_pair(gpu_lib, oracle_lib, frames[:271], window_size=5)
+
+
 def test_of_parity_random_frames(gpu_lib, oracle_lib):
     rng = np.random.default_rng(11)
     _run_pair(gpu_lib, oracle_lib, rng.integers(0, 256, (4, 96, 128, 3), dtype=np.uint8), flow_threshold=2.0)
