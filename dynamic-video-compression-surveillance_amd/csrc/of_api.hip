@@ -280,6 +280,8 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         for (int q = 0; q < 2; ++q)
             if ((e = of_alloc(h, &lv.flow[q], 8 * px * mb)) != hipSuccess) return bad(e, "hipMalloc");
         if (k > 0 && (e = of_alloc(h, &lv.tmpc, 4 * H * 2 * (size_t)lv.w * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if (k > 0 && (e = of_alloc(h, &lv.vtmp, 4 * 2 * (size_t)lv.h * 2 * lv.w * mb)) != hipSuccess)
+            return bad(e, "hipMalloc");
     }
     dvc::OfBufs& b = h->b;
     struct { void** ptr; size_t bytes; } allocs[] = {

@@ -49,6 +49,7 @@ struct Level {
     const LinTap* yt;  // h entries
     float* R;          // ring of RS slots x w*h*5 floats
     float* tmpc;       // level > 0: n x H x 2w horizontal blur sums at the needed columns
+    float* vtmp;       // level > 0: n x 2h x 2w blurred values at the needed (row, column) pairs
     float* flow[2];    // ping-pong n x w*h*2 floats
     const LinTap* ux;  // upsample of the coarser level's flow (k < L): w / h entries
     const LinTap* uy;

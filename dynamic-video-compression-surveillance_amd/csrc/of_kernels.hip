@@ -179,24 +179,46 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 // ----------------------------------------------------------- level k > 0 ----
 // Horizontal smoothing pass (oc_blur_f32, first loop) of the full-resolution
 // gray at the 2w source columns the resize reads: tmpc[y][2dx] at xt[dx].s0,
-// tmpc[y][2dx+1] at xt[dx].s1.
+// tmpc[y][2dx+1] at xt[dx].s1. One workgroup per (row, frame), the gray row
+// staged in LDS (dynamic, W bytes; W % 8 == 0).
 __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
 {
-    const int j = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, t = blockIdx.z;
-    const int W = g.W, H = g.H;
-    if (j >= 2 * lv.w) return;
-    const LinTap tp = lv.xt[j >> 1];
-    const int c = (j & 1) ? tp.s1 : tp.s0;
-    const uint8_t* s = gray + (size_t)t * W * H + (size_t)y * W;
-    const int r = lv.r;
-    float acc = lv.kf[r] * (float)s[c];
-    for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
-    lv.tmpc[(size_t)t * H * 2 * lv.w + (size_t)y * 2 * lv.w + j] = acc;
+    extern __shared__ uint32_t srow[];
+    const int y = blockIdx.x, t = blockIdx.y, W = g.W, H = g.H;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(gray + (size_t)t * W * H + (size_t)y * W);
+    for (int i = threadIdx.x; i < W / 4; i += 256) srow[i] = s32[i];
+    __syncthreads();
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(srow);
+    const int r = lv.r, n2 = 2 * lv.w;
+    float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
+    for (int j = threadIdx.x; j < n2; j += 256) {
+        const LinTap tp = lv.xt[j >> 1];
+        const int c = (j & 1) ? tp.s1 : tp.s0;
+        float acc = lv.kf[r] * (float)s[c];
+        for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
+        out[j] = acc;
+    }
 }
 
-// Vertical smoothing pass at the rows the resize reads, the INTER_LINEAR
-// combination (oc_resize_linear_f32) over tile + PN halo, then the polynomial
-// expansion of the level image.
+// Vertical smoothing pass (oc_blur_f32, second loop) at the 2h source rows the
+// resize reads: vtmp[2dy][j] at row yt[dy].s0, vtmp[2dy+1][j] at yt[dy].s1, for
+// every column slot j of tmpc — each blurred value the resize needs, once.
+__global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
+{
+    const int j = blockIdx.x * 256 + threadIdx.x, yy = blockIdx.y, t = blockIdx.z;
+    const int H = g.H, n2 = 2 * lv.w, r = lv.r;
+    if (j >= n2) return;
+    const LinTap ty = lv.yt[yy >> 1];
+    const int row = (yy & 1) ? ty.s1 : ty.s0;
+    const float* T = lv.tmpc + (size_t)t * H * n2 + j;
+    float acc = lv.kf[r] * T[(size_t)row * n2];
+    for (int i = 1; i <= r; ++i)
+        acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
+    lv.vtmp[((size_t)t * 2 * lv.h + yy) * n2 + j] = acc;
+}
+
+// The INTER_LINEAR combination (oc_resize_linear_f32) over tile + PN halo from
+// vtmp, then the polynomial expansion of the level image.
 template <int PN>
 __global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long a0)
 {
@@ -204,25 +226,18 @@ __global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long 
     __shared__ float sI[IH * IW];
     __shared__ float sv[PT_H * IW * 3];
     const int tid = threadIdx.x, t = blockIdx.z;
-    const int H = g.H, w = lv.w, h = lv.h, r = lv.r;
+    const int w = lv.w, h = lv.h, n2 = 2 * w;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
-    const float* T = lv.tmpc + (size_t)t * H * 2 * w;
-    const size_t TS = 2 * (size_t)w;
-    auto vblur = [&](int row, int col) {   // blurred full-res value at (row, source column slot col)
-        float acc = lv.kf[r] * T[(size_t)row * TS + col];
-        for (int i = 1; i <= r; ++i)
-            acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * TS + col] + T[(size_t)reflect101(row + i, H) * TS + col]);
-        return acc;
-    };
+    const float* V = lv.vtmp + (size_t)t * 2 * h * n2;
     for (int idx = tid; idx < IH * IW; idx += 256) {
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 - PN + i, x = x0 - PN + j;
         if (y < 0 || y >= h || x < 0 || x >= w) continue;
         const LinTap ty = lv.yt[y], tx = lv.xt[x];
-        const float v00 = vblur(ty.s0, 2 * x), v01 = vblur(ty.s0, 2 * x + 1);
-        const float v10 = vblur(ty.s1, 2 * x), v11 = vblur(ty.s1, 2 * x + 1);
-        const float t0 = v00 * tx.w0 + v01 * tx.w1;
-        const float t1 = v10 * tx.w0 + v11 * tx.w1;
+        const float* v0 = V + (size_t)(2 * y) * n2 + 2 * x;
+        const float* v1 = v0 + n2;
+        const float t0 = v0[0] * tx.w0 + v0[1] * tx.w1;
+        const float t1 = v1[0] * tx.w0 + v1[1] * tx.w1;
         sI[idx] = t0 * ty.w0 + t1 * ty.w1;
     }
     __syncthreads();
@@ -924,8 +939,8 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
         else hipLaunchKernelGGL(k_of_front0<7>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
     }
     for (int k = 1; k <= g.L; ++k) {
-        dim3 gh((2 * lv[k].w + 255) / 256, g.H, n);
-        hipLaunchKernelGGL(k_pyr_h, gh, dim3(256), 0, s, g, lv[k], b.gray);
+        hipLaunchKernelGGL(k_pyr_h, dim3(g.H, n), dim3(256), (size_t)g.W, s, g, lv[k], b.gray);
+        hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, 2 * lv[k].h, n), dim3(256), 0, s, g, lv[k]);
         dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);
         if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, s, g, lv[k], a0);
         else hipLaunchKernelGGL(k_pyr_poly<7>, gp, dim3(256), 0, s, g, lv[k], a0);
