@@ -88,27 +88,28 @@ __device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0
         v[2] = r2;
     }
     __syncthreads();
-    // horizontal part, double; replicated row ends
+    // horizontal part (oc_poly_exp): float sub-expressions widened into double
+    // accumulators, only tg * g / tg * xxg double products; replicated row ends
     for (int idx = tid; idx < PT_H * PT_W; idx += 256) {
         const int i = idx / PT_W, jx = idx - i * PT_W;
         const int y = y0 + i, x = x0 + jx;
         if (y >= h || x >= w) continue;
         const float* c = sv + (i * IW + jx + PN) * 3;
-        const double gc = (double)pc.g[PN];
-        double b1 = (double)c[0] * gc, b2 = 0, b3 = (double)c[1] * gc, b4 = 0;
-        double b5 = (double)c[2] * gc, b6 = 0;
+        const float gc = pc.g[PN];
+        double b1 = (double)(c[0] * gc), b2 = 0, b3 = (double)(c[1] * gc), b4 = 0;
+        double b5 = (double)(c[2] * gc), b6 = 0;
 #pragma unroll
         for (int k = 1; k <= PN; ++k) {
             const float* P = sv + (i * IW + (min(x + k, w - 1) - (x0 - PN))) * 3;
             const float* M = sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
-            const double gk = (double)pc.g[PN + k], xgk = (double)pc.xg[PN + k], xxgk = (double)pc.xxg[PN + k];
-            const double tg = (double)P[0] + (double)M[0];
-            b1 += tg * gk;
-            b4 += tg * xxgk;
-            b2 += ((double)P[0] - (double)M[0]) * xgk;
-            b3 += ((double)P[1] + (double)M[1]) * gk;
-            b6 += ((double)P[1] - (double)M[1]) * xgk;
-            b5 += ((double)P[2] + (double)M[2]) * gk;
+            const float gk = pc.g[PN + k], xgk = pc.xg[PN + k];
+            const double tg = (double)(P[0] + M[0]);
+            b1 += tg * (double)gk;
+            b4 += tg * (double)pc.xxg[PN + k];
+            b2 += (double)((P[0] - M[0]) * xgk);
+            b3 += (double)((P[1] + M[1]) * gk);
+            b6 += (double)((P[1] - M[1]) * xgk);
+            b5 += (double)((P[2] + M[2]) * gk);
         }
         float* d = R + ((size_t)y * w + x) * 5;
         d[1] = (float)(b2 * pc.ig11);

@@ -181,17 +181,29 @@ void oc_poly_exp(const float* src, int W, int H, int n, double sigma, float* dst
             r[3 * W + x] = r[3 * W + x - 3];
         }
         float* d = dst + (size_t)y * W * 5;
+        /* Horizontal part with the C++ types of FarnebackPolyExp: row, g, xg,
+         * xxg are float, b1..b6 double. So `row*g0`, `row[a] + row[b]` and
+         * `(row[a] -/+ row[b]) * xg[k]` (both operands float) round in float
+         * before widening; only `tg * g0` and `tg * xxg[k]` (tg double) are
+         * double products. */
         for (int x = 0; x < W; ++x) {
-            double b1 = (double)r[3 * x] * g[n], b2 = 0, b3 = (double)r[3 * x + 1] * g[n], b4 = 0;
-            double b5 = (double)r[3 * x + 2] * g[n], b6 = 0;
+            const float c0 = r[3 * x] * g[n], c1 = r[3 * x + 1] * g[n], c2 = r[3 * x + 2] * g[n];
+            double b1 = c0, b2 = 0, b3 = c1, b4 = 0, b5 = c2, b6 = 0;
             for (int k = 1; k <= n; ++k) {
-                double tg = (double)r[3 * (x + k)] + (double)r[3 * (x - k)];
+                const float* P = r + 3 * (x + k);
+                const float* M = r + 3 * (x - k);
+                const float tgf = P[0] + M[0];
+                const double tg = tgf;
                 b1 += tg * g[n + k];
                 b4 += tg * xxg[n + k];
-                b2 += ((double)r[3 * (x + k)] - (double)r[3 * (x - k)]) * xg[n + k];
-                b3 += ((double)r[3 * (x + k) + 1] + (double)r[3 * (x - k) + 1]) * g[n + k];
-                b6 += ((double)r[3 * (x + k) + 1] - (double)r[3 * (x - k) + 1]) * xg[n + k];
-                b5 += ((double)r[3 * (x + k) + 2] + (double)r[3 * (x - k) + 2]) * g[n + k];
+                const float q2 = (P[0] - M[0]) * xg[n + k];
+                const float q3 = (P[1] + M[1]) * g[n + k];
+                const float q6 = (P[1] - M[1]) * xg[n + k];
+                const float q5 = (P[2] + M[2]) * g[n + k];
+                b2 += q2;
+                b3 += q3;
+                b6 += q6;
+                b5 += q5;
             }
             d[5 * x + 1] = (float)(b2 * ig[0]);
             d[5 * x] = (float)(b3 * ig[0]);
