@@ -132,9 +132,12 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
                                                    const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
                                                    long long a0)
 {
-    constexpr int HG = PN + 1, GW = PT_W + 2 * HG, GH = PT_H + 2 * HG;
+    // gray tile: rows y0-HG .., columns from x0-GX in whole 4-px quads (GX = 8 >= HG
+    // keeps each quad's 12 BGR bytes 4-byte aligned: x0 % 64 == 0, pitch % 4 == 0)
+    constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG, NQ = GW / 4;
     constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
-    __shared__ float sg[GH * GW];
+    static_assert(HG <= GX, "halo wider than the quad pad");
+    __shared__ __attribute__((aligned(16))) float sg[GH * GW];
     __shared__ float sI[IH * IW];
     __shared__ float sv[PT_H * IW * 3];
     const int tid = threadIdx.x, t = blockIdx.z;
@@ -142,14 +145,16 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     const uint8_t* f = bgr + (size_t)t * fstride;
     uint8_t* go = gray_out + (size_t)t * W * H;
-    for (int idx = tid; idx < GH * GW; idx += 256) {
-        const int i = idx / GW, j = idx - i * GW;
-        const int y = y0 - HG + i, x = x0 - HG + j;
-        if (y < 0 || y >= H || x < 0 || x >= W) continue;
-        const uint8_t* p = f + (size_t)y * pitch + 3 * x;
-        const uint32_t v = gray_px(p[0], p[1], p[2]);
-        sg[idx] = (float)v;
-        if (i >= HG && i < HG + PT_H && j >= HG && j < HG + PT_W) go[(size_t)y * W + x] = (uint8_t)v;
+    for (int idx = tid; idx < GH * NQ; idx += 256) {
+        const int i = idx / NQ, q = idx - i * NQ;
+        const int y = y0 - HG + i, px = x0 - GX + 4 * q;
+        if (y < 0 || y >= H || px < 0 || px >= W) continue;   // W % 8 == 0: quads are whole
+        const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)y * pitch + 3 * px);
+        const uint32_t gq = gray4_dot(v.x, v.y, v.z);   // of:71 BGR2GRAY of 4 px
+        *reinterpret_cast<float4*>(sg + i * GW + 4 * q) =
+            make_float4((float)(gq & 255), (float)((gq >> 8) & 255), (float)((gq >> 16) & 255), (float)(gq >> 24));
+        if (i >= HG && i < HG + PT_H && px >= x0 && px < x0 + PT_W)
+            *reinterpret_cast<uint32_t*>(go + (size_t)y * W + px) = gq;
     }
     __syncthreads();
     // I = blur3(gray): horizontal pass at the 3 rows, then vertical (oc_blur_f32)
@@ -158,7 +163,7 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 - PN + i, x = x0 - PN + j;
         if (y < 0 || y >= H || x < 0 || x >= W) continue;
-        const int xl = reflect1(x - 1, W) - (x0 - HG), xc = x - (x0 - HG), xr = reflect1(x + 1, W) - (x0 - HG);
+        const int xl = reflect1(x - 1, W) - (x0 - GX), xc = x - (x0 - GX), xr = reflect1(x + 1, W) - (x0 - GX);
         float hv[3];
         const int ys[3] = {reflect1(y - 1, H), y, reflect1(y + 1, H)};
 #pragma unroll
