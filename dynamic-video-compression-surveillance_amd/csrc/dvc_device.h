@@ -59,6 +59,15 @@ __device__ __forceinline__ uint32_t gray4_dot(uint32_t d0, uint32_t d1, uint32_t
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
+// Order LDS accesses of the lanes of ONE wave (no workgroup barrier): for
+// exchanges confined to a wave's own LDS slice.
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t ald(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

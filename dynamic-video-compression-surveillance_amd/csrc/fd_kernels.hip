@@ -390,13 +390,8 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
 }
 
 // Contour-filter kernels after k_band give each row (seam) a group of lanes of
-// its own and synchronise only within the wave (each group its own LDS slice).
-__device__ __forceinline__ void wave_sync_lds()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// its own and synchronise only within the wave (each group its own LDS slice,
+// wave_sync_lds in dvc_device.h).
 
 // ------------------------------------------------------------------ merge ---
 // One group of MG lanes per band seam (rows b*BH-1 and b*BH): run indexes of

@@ -777,113 +777,145 @@ __global__ void __launch_bounds__(256) k_of_rect(OfGeom g, OfBufs B)
     }
 }
 
-// ----------------------------------------------------------------- output ---
-// One lane per 8x8 block (64 blocks across, one wave per block row, 4 block
-// rows per workgroup), blockIdx.z = frame. compress_with_motion (of:151-183):
-// BGR->YCrCb (of:152); a full block whose mask is all zero (of:159,161) gets
-// each of Y, Cr, Cb DCT-quantised (of:162-168); all pixels YCrCb->BGR
-// (of:170-171); static blocks then BGR->gray->BGR (of:174-183).
+// k_of_out: one group of 8 lanes per 8x8 block (lane r = row r of the block),
+// 8 blocks side by side per wave (64 px x 8 rows), 4 waves = 4 block rows.
+// Per static full block and channel (of:156-168) the separable DCT, quantiser
+// and IDCT of block_dct_quant<8> — same dot products, same operation order —
+// with row passes in the lane's registers and column passes after 8x8
+// transposes through LDS (rows padded to 9 floats: conflict-free); a group
+// only ever exchanges data within its own wave, so wave-level ordering suffices.
+// Small per-lane state: many waves per SIMD instead of one 270-VGPR wave.
+__device__ __forceinline__ void dct_rows8(const float (&x)[8], const DctMat& M, float (&y)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // y[k] = sum_n x[n] M[k][n]
+        float t = x[0] * M.m[k * 8];
+#pragma unroll
+        for (int n = 1; n < 8; ++n) t = __builtin_fmaf(x[n], M.m[k * 8 + n], t);
+        y[k] = t;
+    }
+}
+
+__device__ __forceinline__ void idct_rows8(const float (&x)[8], const DctMat& M, float (&y)[8])
+{
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {   // y[n] = sum_l x[l] M[l][n]
+        float t = x[0] * M.m[n];
+#pragma unroll
+        for (int l = 1; l < 8; ++l) t = __builtin_fmaf(x[l], M.m[l * 8 + n], t);
+        y[n] = t;
+    }
+}
+
+// S: the group's 8 x 9 tile. Lane r stores v as row r and returns column r.
+__device__ __forceinline__ void transpose8(float* S, int r, const float (&v)[8], float (&out)[8])
+{
+    wave_sync_lds();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) S[r * 9 + k] = v[k];
+    wave_sync_lds();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = S[i * 9 + r];
+}
+
 __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
 {
+    __shared__ float sT[4][8][72];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = blockIdx.z;
     const int W = g.W, H = g.H, WW = g.WW;
-    const int bx = (blockIdx.x * 64 + lane) * 8, by = (blockIdx.y * 4 + wave) * 8;
-    if (bx >= W || by >= H) return;
-    const uint8_t* f = o.bgr + (size_t)t * o.fstride;
+    const int gb = lane >> 3, r = lane & 7;
+    const int bx = (blockIdx.x * 8 + gb) * 8, by = (blockIdx.y * 4 + wave) * 8, y = by + r;
+    const bool act = bx < W && y < H;
+    float* S = sT[wave][gb];
     const uint64_t* rb = B.rbits + (size_t)t * H * WW;
-    uint32_t mrow[8];
-    uint32_t any = 0;
+    const uint32_t mrow = act ? (uint32_t)(rb[(size_t)y * WW + (bx >> 6)] >> (bx & 63)) & 0xffu : 0u;
+    uint32_t any = mrow;
+    any |= __shfl_xor(any, 1, 8);
+    any |= __shfl_xor(any, 2, 8);
+    any |= __shfl_xor(any, 4, 8);
+    if (o.mask && act) {
+        uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        mrow[i] = (uint32_t)(rb[(size_t)(by + i) * WW + (bx >> 6)] >> (bx & 63)) & 0xffu;
-        any |= mrow[i];
-    }
-    if (o.mask) {
-        uint8_t* mk = o.mask + (size_t)t * o.mstride;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                lo |= ((mrow[i] >> j) & 1u) ? (255u << (8 * j)) : 0u;
-                hi |= ((mrow[i] >> (j + 4)) & 1u) ? (255u << (8 * j)) : 0u;
-            }
-            *reinterpret_cast<uint2*>(mk + (size_t)(by + i) * W + bx) = make_uint2(lo, hi);
+        for (int j = 0; j < 4; ++j) {
+            lo |= ((mrow >> j) & 1u) ? (255u << (8 * j)) : 0u;
+            hi |= ((mrow >> (j + 4)) & 1u) ? (255u << (8 * j)) : 0u;
         }
+        *reinterpret_cast<uint2*>(o.mask + (size_t)t * o.mstride + (size_t)y * W + bx) = make_uint2(lo, hi);
     }
     if (!o.compressed) return;
-    const bool is_static = any == 0;
-    // YCrCb planes of the block, 8 px per row as two u32 per channel
-    uint32_t yc[3][8][2];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * o.pitch + 3 * bx);
+    // this lane's row of the block: BGR -> YCrCb (of:156)
+    int ch[3][8];
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(o.bgr + (size_t)t * o.fstride +
+                                                               (size_t)(act ? y : 0) * o.pitch + 3 * (act ? bx : 0));
         uint32_t px[6];
 #pragma unroll
         for (int d = 0; d < 6; ++d) px[d] = src[d];
-        uint32_t Y[2] = {0, 0}, Cr[2] = {0, 0}, Cb[2] = {0, 0};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int b = (px[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
             const int gg = (px[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
-            const int r = (px[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
-            const int yv = descale14(b * 1868 + gg * 9617 + r * 4899);
-            const uint32_t cr = satu8(descale14((r - yv) * 11682 + (128 << 14)));
-            const uint32_t cb = satu8(descale14((b - yv) * 9241 + (128 << 14)));
-            Y[j >> 2] |= (uint32_t)yv << (8 * (j & 3));
-            Cr[j >> 2] |= cr << (8 * (j & 3));
-            Cb[j >> 2] |= cb << (8 * (j & 3));
+            const int rr = (px[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+            const int yv = descale14(b * 1868 + gg * 9617 + rr * 4899);
+            ch[0][j] = yv;
+            ch[1][j] = (int)satu8(descale14((rr - yv) * 11682 + (128 << 14)));
+            ch[2][j] = (int)satu8(descale14((b - yv) * 9241 + (128 << 14)));
         }
-        yc[0][i][0] = Y[0]; yc[0][i][1] = Y[1];
-        yc[1][i][0] = Cr[0]; yc[1][i][1] = Cr[1];
-        yc[2][i][0] = Cb[0]; yc[2][i][1] = Cb[1];
     }
-    const bool full = bx + 8 <= W && by + 8 <= H;
-    if (is_static && full) {
+    const bool sfull = any == 0 && bx + 8 <= W && by + 8 <= H;   // uniform per group
+    if (sfull) {   // of:158-168, Y, Cr and Cb
+        auto channel = [&](int (&cc)[8]) {
+            float x[8], v[8], u[8];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            float X[64];
+            for (int j = 0; j < 8; ++j) x[j] = (float)cc[j] - 128.0f;
+            dct_rows8(x, o.M, v);            // T row r
+            transpose8(S, r, v, u);          // T column r: u[i] = T[i][r]
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int k = 0; k < 8; ++k) {    // X[k][r] = rint(sum_i M[k][i] T[i][r] / q) q
+                float tt = o.M.m[k * 8] * u[0];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) X[i * 8 + j] = (float)((yc[c][i][j >> 2] >> (8 * (j & 3))) & 255) - 128.0f;
-            block_dct_quant<8>(X, o.M, o.quant, o.qinv);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                uint32_t v2[2] = {0, 0};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    float v = X[i * 8 + j] + 128.0f;
-                    v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
-                    v2[j >> 2] |= ((uint32_t)v & 255u) << (8 * (j & 3));
-                }
-                yc[c][i][0] = v2[0];
-                yc[c][i][1] = v2[1];
+                for (int i = 1; i < 8; ++i) tt = __builtin_fmaf(o.M.m[k * 8 + i], u[i], tt);
+                v[k] = __builtin_rintf(div_rn(tt, o.qinv)) * o.quant;
             }
-        }
+            transpose8(S, r, v, x);          // X row r
+            idct_rows8(x, o.M, v);           // T2 row r
+            transpose8(S, r, v, u);          // T2 column r
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {    // X[i][r] = sum_k M[k][i] T2[k][r]
+                float tt = o.M.m[i] * u[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k) tt = __builtin_fmaf(o.M.m[k * 8 + i], u[k], tt);
+                v[i] = tt;
+            }
+            transpose8(S, r, v, x);          // row r of the reconstruction
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {    // np.clip + truncating uint8 assignment
+                float f = x[j] + 128.0f;
+                f = f < 0.f ? 0.f : (f > 255.f ? 255.f : f);
+                cc[j] = (int)((uint32_t)f & 255u);
+            }
+        };
+        channel(ch[0]);
+        channel(ch[1]);
+        channel(ch[2]);
     }
-    uint8_t* cpf = o.compressed + (size_t)t * o.ostride;
+    if (!act) return;
+    uint8_t ob[24];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint8_t ob[24];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int yv = (yc[0][i][j >> 2] >> (8 * (j & 3))) & 255;
-            const int cr = (int)((yc[1][i][j >> 2] >> (8 * (j & 3))) & 255) - 128;
-            const int cb = (int)((yc[2][i][j >> 2] >> (8 * (j & 3))) & 255) - 128;
-            uint32_t b = satu8(yv + descale14(cb * 29049));
-            uint32_t gg = satu8(yv + descale14(cb * -5636 + cr * -11698));
-            uint32_t r = satu8(yv + descale14(cr * 22987));
-            if (is_static && full) b = gg = r = gray_px(b, gg, r);
-            ob[3 * j] = (uint8_t)b;
-            ob[3 * j + 1] = (uint8_t)gg;
-            ob[3 * j + 2] = (uint8_t)r;
-        }
-        uint32_t* d = reinterpret_cast<uint32_t*>(cpf + (size_t)(by + i) * 3 * W + 3 * bx);
-#pragma unroll
-        for (int q = 0; q < 6; ++q)
-            d[q] = ob[4 * q] | (ob[4 * q + 1] << 8) | (ob[4 * q + 2] << 16) | ((uint32_t)ob[4 * q + 3] << 24);
+    for (int j = 0; j < 8; ++j) {   // YCrCb -> BGR (of:170-171); static blocks -> gray -> BGR (of:174-183)
+        const int yv = ch[0][j], cr = ch[1][j] - 128, cb = ch[2][j] - 128;
+        uint32_t b = satu8(yv + descale14(cb * 29049));
+        uint32_t gg = satu8(yv + descale14(cb * -5636 + cr * -11698));
+        uint32_t rr = satu8(yv + descale14(cr * 22987));
+        if (sfull) b = gg = rr = gray_px(b, gg, rr);
+        ob[3 * j] = (uint8_t)b;
+        ob[3 * j + 1] = (uint8_t)gg;
+        ob[3 * j + 2] = (uint8_t)rr;
     }
+    uint32_t* d = reinterpret_cast<uint32_t*>(o.compressed + (size_t)t * o.ostride + (size_t)y * 3 * W + 3 * bx);
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+        d[q] = ob[4 * q] | (ob[4 * q + 1] << 8) | (ob[4 * q + 2] << 16) | ((uint32_t)ob[4 * q + 3] << 24);
 }
 
 // Static-block counter (separate tiny pass keeps k_of_out's exits simple).
@@ -1015,7 +1047,7 @@ hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int wi
 hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s)
 {
     if (!o.mask && !o.compressed) return hipSuccess;
-    dim3 grid((g.W / 8 + 63) / 64, (g.H / 8 + 3) / 4, n);
+    dim3 grid((g.W / 8 + 7) / 8, (g.H / 8 + 3) / 4, n);
     hipLaunchKernelGGL(k_of_out, grid, dim3(256), 0, s, g, b, o);
     return hipGetLastError();
 }
