@@ -113,11 +113,22 @@ int vote_threshold(double alpha, int L)
 
 }  // namespace
 
+// Events of one batch in flight; two slots alternate (batch i waits on i-2).
+struct OfSlot {
+    hipEvent_t ev_pyr = nullptr, ev_flow = nullptr, ev_mask = nullptr;
+    bool recorded = false;
+};
+
 struct dvc_of {
     dvc_of_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // prime + pyramid stage (s_pyr); the caller's stream if given
     bool own_stream = false;
+    // batch i: s_pyr [wait flow(i-2)] pyramid(i); s_flow [wait pyramid(i),
+    // mask(i-2)] flow(i); s_mask [wait flow(i)] vote/morphology/rects + out(i)
+    hipStream_t s_pyr = nullptr, s_flow = nullptr, s_mask = nullptr;
+    OfSlot slot[2];
+    uint64_t seq = 0;
     dvc::OfGeom g{};
     dvc::Level lv[dvc::OF_MAX_LEVELS]{};
     dvc::OfBufs b{};
@@ -142,7 +153,20 @@ static void of_free(dvc_of* h)
     for (void* p : {(void*)h->h_in, (void*)h->h_mask, (void*)h->h_cp})
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    for (OfSlot& sl : h->slot)
+        for (hipEvent_t e : {sl.ev_pyr, sl.ev_flow, sl.ev_mask})
+            if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {h->s_flow, h->s_mask})
+        if (st) (void)hipStreamDestroy(st);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+static hipError_t of_sync_all(dvc_of* h)
+{
+    hipError_t e = hipStreamSynchronize(h->stream);
+    for (hipStream_t st : {h->s_flow, h->s_mask})
+        if (e == hipSuccess && st) e = hipStreamSynchronize(st);
+    return e;
 }
 
 template <typename T>
@@ -199,8 +223,11 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     g.WW = (p.width + 63) / 64;
     g.CAP = p.width / 2 + 1;
     g.L = L;
-    g.RS = mb + 1;
-    g.RB = p.window + mb;
+    // rings sized for two batches in flight: the pyramid of batch i+1 and the
+    // flow of batch i (R: frames a0-1 .. a0+2n-1), the flow of batch i+1 and
+    // the vote of batch i (raw bits: frames a0-window .. a0+2n-1)
+    g.RS = 2 * mb + 1;
+    g.RB = p.window + 2 * mb;
     g.iters = p.iterations;
     g.m = p.winsize / 2;
     g.box_scale = 1. / (p.winsize * p.winsize);
@@ -229,6 +256,15 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
         h->own_stream = true;
     }
+    // three streams in all (the handle's own carries the pyramid): within the
+    // default 4 hardware queues beside the framework's stream, so no two stages
+    // share a queue (a shared queue serialises them)
+    h->s_pyr = h->stream;
+    for (hipStream_t* st : {&h->s_flow, &h->s_mask})
+        if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (OfSlot& sl : h->slot)
+        for (hipEvent_t* ev : {&sl.ev_pyr, &sl.ev_flow, &sl.ev_mask})
+            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = g.WW, CAP = g.CAP;
     // levels (oc_fb_level_poly geometry)
     std::vector<dvc::LinTap> tabs;   // all tables, uploaded once
@@ -331,7 +367,7 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
     if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));   // no batch of a previous run may still be in flight
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
     const uint8_t* d = bgr;
     int dp = (int)pitch;
@@ -346,6 +382,8 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     HIP_OK(hipMemsetAsync(h->b.cnt, 0, 64 * H * WW, h->stream));
     HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
+    for (OfSlot& sl : h->slot) sl.recorded = false;
+    h->seq = 0;
     h->a_next = 1;
     h->frames = 0;
     h->last_n = 0;
@@ -360,7 +398,15 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
 {
     const long long a0 = h->a_next;
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->stream));
+    // slot S last held batch i-2: with RS = 2 mb + 1 the pyramid of batch i
+    // overwrites R slots that only flow(i-2) reads; with RB = window + 2 mb the
+    // raw bits flow(i) writes are the evictions only vote(i-2) reads
+    OfSlot& S = h->slot[h->seq & 1];
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->s_pyr));
+    HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
+    HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_pyr, 0));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_mask, 0));
     if (timed) {
         while (h->ev.size() < h->ev_used + 2) {
             hipEvent_t e;
@@ -368,14 +414,16 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->stream));
-    if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->stream));
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->stream));
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow));
+    if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_flow));
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow));
     if (timed) {
-        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->stream));
+        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_flow));
         h->ev_used += 2;
     }
-    HIP_OK(dvc::of_launch_mask(h->g, h->b, a0, h->p.window, n, h->stream));
+    HIP_OK(hipEventRecord(S.ev_flow, h->s_flow));
+    HIP_OK(hipStreamWaitEvent(h->s_mask, S.ev_flow, 0));
+    HIP_OK(dvc::of_launch_mask(h->g, h->b, a0, h->p.window, n, h->s_mask));
     dvc::OfOutArgs o{};
     o.bgr = d;
     o.pitch = dp;
@@ -387,7 +435,10 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     o.quant = h->p.quant;
     o.qinv = 1.0 / (double)h->p.quant;
     o.M = h->M;
-    HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->stream));
+    HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->s_mask));
+    HIP_OK(hipEventRecord(S.ev_mask, h->s_mask));
+    S.recorded = true;
+    h->seq++;
     h->a_next += n;
     h->frames += (uint64_t)n;
     h->last_n = n;
@@ -422,12 +473,12 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
         for (int t = 0; t < m; ++t)
             for (size_t y = 0; y < H; ++y)
                 std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->stream));
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_pyr));
         int rc = of_enqueue(h, h->d_in, (int)row, 3 * N, m, mk ? h->d_mask : nullptr, N, cp ? h->d_cp : nullptr, 3 * N);
         if (rc) return rc;
-        if (mk) HIP_OK(hipMemcpyAsync(h->h_mask, h->d_mask, (size_t)m * N, hipMemcpyDeviceToHost, h->stream));
-        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->stream));
-        HIP_OK(hipStreamSynchronize(h->stream));
+        if (mk) HIP_OK(hipMemcpyAsync(h->h_mask, h->d_mask, (size_t)m * N, hipMemcpyDeviceToHost, h->s_mask));
+        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_mask));
+        HIP_OK(of_sync_all(h));
         for (int t = 0; t < m; ++t) {
             if (mk) std::memcpy(mk + (size_t)t * mstride, h->h_mask + (size_t)t * N, N);
             if (cp) std::memcpy(cp + (size_t)t * ostride, h->h_cp + (size_t)t * 3 * N, 3 * N);
@@ -453,7 +504,7 @@ int dvc_of_sync(dvc_of* h)
 {
     if (!h) return fail(DVC_E_INVALID, "NULL handle");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     return DVC_OK;
 }
 
@@ -461,7 +512,7 @@ int dvc_of_get_stats(dvc_of* h, dvc_of_stats* out)
 {
     if (!h || !out) return fail(DVC_E_INVALID, "NULL argument");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     unsigned long long slots[64 * 4], s[4] = {0, 0, 0, 0};
     HIP_OK(hipMemcpy(slots, h->b.stats, sizeof(slots), hipMemcpyDeviceToHost));
     for (int i = 0; i < 64 * 4; ++i) s[i % 4] += slots[i];
@@ -477,7 +528,7 @@ int dvc_of_read_plane(dvc_of* h, int plane, uint8_t* dst)
     if (!h || !dst) return fail(DVC_E_INVALID, "NULL argument");
     if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW, t = (size_t)h->last_n - 1;
     if (plane == DVC_OF_PLANE_GRAY) {
         HIP_OK(hipMemcpy(dst, h->b.gray + t * N, N, hipMemcpyDeviceToHost));
@@ -504,7 +555,7 @@ int dvc_of_read_flow(dvc_of* h, float* dst)
     if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
     if (!h->b.dbg_flow) return fail(DVC_E_STATE, "flow readback needs DVC_FLAG_KEEP_PLANES");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     HIP_OK(hipMemcpy(dst, h->b.dbg_flow, 8 * (size_t)h->p.width * h->p.height, hipMemcpyDeviceToHost));
     return DVC_OK;
 }
@@ -513,7 +564,7 @@ int dvc_of_ktime(dvc_of* h, double* total_ms, uint64_t* launches, int reset)
 {
     if (!h) return fail(DVC_E_INVALID, "NULL handle");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     double t = 0.0;
     for (size_t i = 0; i + 1 < h->ev_used; i += 2) {
         float ms = 0.f;
@@ -536,7 +587,7 @@ int dvc_of_debug_read(dvc_of* h, int what, int level, void* dst, int* w, int* hg
     if (!dst) return DVC_OK;
     if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
     HIP_OK(hipSetDevice(h->device));
-    HIP_OK(hipStreamSynchronize(h->stream));
+    HIP_OK(of_sync_all(h));
     const size_t px = (size_t)L.w * L.h;
     const long long a = h->a_next - 1;
     const void* src = nullptr;
@@ -559,7 +610,7 @@ void dvc_of_destroy(dvc_of* h)
 {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    (void)hipStreamSynchronize(h->stream);
+    (void)of_sync_all(h);
     of_free(h);
     delete h;
 }

@@ -228,8 +228,10 @@ typedef struct dvc_of_stats {
 /* Create an OF feed handle on `device` (GPU constraints: width and height
  * multiples of 8, morph_kernel 2, poly_n 5 or 7, winsize <= 17, window <= 127,
  * pyramid smoothing kernels <= 63 taps). Replaces the per-video setup at
- * of:38-62. All launches go to `hip_stream` (NULL: a stream owned by the
- * handle). */
+ * of:38-62. `hip_stream` (NULL: a stream owned by the handle) carries prime and
+ * the gray/pyramid stage; the flow and the vote/morphology/output stages run on
+ * two internal streams with two batches' rings in flight. Device-pointer steps
+ * return after enqueueing: dvc_of_sync (or any read-back call) waits for all. */
 int dvc_of_create(const dvc_of_params* params, int device, void* hip_stream, dvc_of** out);
 
 /* Frame 0: gray (of:60) and its pyramid; the vote window is emptied (of:61). */
