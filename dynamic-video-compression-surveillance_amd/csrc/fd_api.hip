@@ -115,18 +115,15 @@ struct Slot {
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
 };
 
-// Batches in flight: three slots; the contour filter has no recurrence across
-// batches, so consecutive batches may alternate between up to two streams.
-constexpr int NSLOT = 3, NCCL_MAX = 2;
+// Batches in flight: three slots.
+constexpr int NSLOT = 3;
 
 struct dvc_fd {
     dvc_fd_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;  // prime + completion join; the caller's stream if given
+    hipStream_t stream = nullptr;  // prime + contour filter; the caller's stream if given
     bool own_stream = false;
     hipStream_t s_front = nullptr;       // blur/threshold front (previous-gray recurrence)
-    hipStream_t s_ccl[NCCL_MAX] = {};    // contour filter of batch i on s_ccl[i % nccl]
-    int nccl = 1;
     hipStream_t s_acc = nullptr;         // dilate + accumulate (accumulated-mask recurrence)
     hipStream_t s_out = nullptr;         // overlay + compressed frames
     dvc::RowGeom g{};
@@ -172,7 +169,7 @@ static void free_all(dvc_fd* h)
     for (void* p : pin)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-    for (hipStream_t st : {h->s_front, h->s_ccl[0], h->s_ccl[1], h->s_acc, h->s_out})
+    for (hipStream_t st : {h->s_front, h->s_acc, h->s_out})
         if (st) (void)hipStreamDestroy(st);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
 }
@@ -186,7 +183,7 @@ static hipError_t dalloc(T** p, size_t bytes)
 static hipError_t sync_all(dvc_fd* h)
 {
     hipError_t e = hipStreamSynchronize(h->stream);
-    for (hipStream_t st : {h->s_front, h->s_ccl[0], h->s_ccl[1], h->s_acc, h->s_out})
+    for (hipStream_t st : {h->s_front, h->s_acc, h->s_out})
         if (e == hipSuccess && st) e = hipStreamSynchronize(st);
     return e;
 }
@@ -251,20 +248,17 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bad(e, "hipSetDevice");
     if (hip_stream) h->stream = (hipStream_t)hip_stream;
-    // priorities: the latency-bound contour filter and accumulate chains high,
-    // the VALU-bound front low
+    // four streams in all — the handle's (contour filter), front, accumulate,
+    // output — within the default 4 hardware queues (a queue shared by two
+    // stages serialises them); priorities: the latency-bound contour filter and
+    // accumulate chains high, the VALU-bound front low
     int plo = 0, phi = 0;
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
     auto mk = [](hipStream_t* st, int prio) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio); };
     if (!hip_stream) {
-        if ((e = mk(&h->stream, 0)) != hipSuccess) return bad(e, "hipStreamCreate");
+        if ((e = mk(&h->stream, phi)) != hipSuccess) return bad(e, "hipStreamCreate");
         h->own_stream = true;
     }
-    // four internal streams fit the default 4 hardware queues (GPU_MAX_HW_QUEUES);
-    // DVC_CCL_STREAMS=2 adds a second contour-filter stream
-    if (const char* ev = getenv("DVC_CCL_STREAMS")) h->nccl = std::max(1, std::min(NCCL_MAX, atoi(ev)));
-    for (int i = 0; i < h->nccl; ++i)
-        if ((e = mk(&h->s_ccl[i], phi)) != hipSuccess) return bad(e, "hipStreamCreate");
     for (auto sp : {std::make_pair(&h->s_front, plo), std::make_pair(&h->s_acc, phi), std::make_pair(&h->s_out, 0)})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
@@ -351,17 +345,17 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 // Enqueue one batch i of n <= max_batch device-resident frames, slot S = i % 3
 // (j = i - 3 = the slot's previous batch):
 //   s_front:         [wait ccl(j)]            front(i) -> ev_front   (S.mbits free)
-//   s_ccl[i % 2]:    [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
+//   stream:          [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
 //   s_acc:           [wait ev_ccl, out(j)]    dilate + accumulate(i) -> ev_acc (S bits free)
 //   s_out:           [wait ev_acc]            k_out(i) -> ev_out
-// so front(i+2), the contour filters of i+1 and i, the accumulation of i and
-// the output of i-1 can all be in flight; only the two recurrences (previous
-// gray, accumulated mask) are serial, each on its own stream.
+// so front(i+2), the contour filter of i+1, the accumulation of i and the
+// output of i-1 can all be in flight; the two recurrences (previous gray,
+// accumulated mask) are serial, each on its own stream.
 static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride)
 {
     Slot& S = h->slot[h->seq % NSLOT];
-    hipStream_t s_ccl = h->s_ccl[h->seq % h->nccl];
+    hipStream_t s_ccl = h->stream;
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
     HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], S.c.mbits, h->g,
                              h->p.ithresh, h->s_front));

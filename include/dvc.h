@@ -111,10 +111,10 @@ const char* dvc_last_error(void);
 int         dvc_device_count(int* count);
 
 /* Create a feed handle on `device`. `hip_stream` (a hipStream_t, may be NULL for
- * a stream owned by the handle) carries prime. Batches run on four internal
- * streams — the blur/threshold front, the contour filter, dilate + accumulate,
- * and the overlay/compress output — with three batches' buffers in flight;
- * only the two recurrences (previous gray, accumulated mask) are serial.
+ * a stream owned by the handle) carries prime and the contour filter; the
+ * blur/threshold front, dilate + accumulate and the overlay/compress output
+ * run on three internal streams, with three batches' buffers in flight; only
+ * the two recurrences (previous gray, accumulated mask) are serial.
  * Device-pointer steps return after enqueueing: dvc_fd_sync (or any read-back
  * call) waits for all streams. Replaces the per-video setup at fd:56-82. */
 int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
