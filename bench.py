@@ -9,13 +9,16 @@ Workload (BASELINE.json configs[1]): one synthetic 1920x1080 camera feed per
 GPU (seed = rank), the full per-frame worker of frame_differencing.py:91-133 —
 gray, 5x5 blur, absdiff/threshold, contour-area filter, 7x7 dilate,
 accumulation, red overlay, static-block DCT quantisation, YCrCb round trip —
-with the GUI's default kwargs (windows.py:154). Frames are device-resident: 64
-distinct synthetic frames played ping-pong (0..63..1) so every consecutive pair
-is real motion, materialised as one contiguous 126-frame sequence (784 MB,
-beyond the 256 MB Infinity Cache); overlay and compressed outputs go to
-126-frame device buffers. A step = one pass over the 126 frames through
-dvc_fd_step_batch (launches of --batch frames; --per-frame: one dvc_fd_step
-per frame instead).
+with the GUI's default kwargs (windows.py:154). Frames are device-resident: R
+distinct synthetic frames (--ring; FD 192, OF 64) played ping-pong
+(0..R-1..1) so every consecutive pair is real motion, materialised as one
+contiguous (2R-2)-frame sequence (FD: 382 frames, 2.4 GB — far beyond the
+256 MB Infinity Cache); overlay and compressed outputs go to device buffers of
+the same length. A step = one pass over that sequence through
+dvc_fd_step_batch (launches of --batch frames, FD default 191: larger grids
+keep the latency-bound contour filter occupied and amortise the stage
+hand-offs — 63 frames measured 274 k Mpx/s, 191 310 k, 383 316 k; --per-frame:
+one dvc_fd_step per frame instead).
 
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
@@ -64,7 +67,8 @@ def pmc_traffic(path: str, kernel_prefix: str, workload: str, frames_per_launch:
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") != workload or abs(d.get("frames_per_launch", frames_per_launch) - frames_per_launch) > 0.5:
+        fpl = d.get("frames_per_launch")
+        if d.get("workload") != workload or fpl is None or abs(fpl - frames_per_launch) > 0.5:
             return None
         k = d["kernels"][kernel_prefix]
         return float(k["hbm_bytes_per_launch"])
@@ -100,13 +104,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--ring", type=int, default=64)
+    ap.add_argument("--ring", type=int, default=0, help="distinct frames (0: 192 fd / 64 of)")
     ap.add_argument("--noisy", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=("fd", "of"), default="fd",
                     help="fd: frame_differencing.py worker (headline); of: motion_compression_opt.py worker")
-    ap.add_argument("--batch", type=int, default=0, help="frames per device launch (max_batch; 0: 63 fd / 16 of)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per device launch (max_batch; 0: 191 fd / 16 of)")
     ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
     args = ap.parse_args()
 
@@ -125,7 +129,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    W, H, R = args.width, args.height, args.ring
+    W, H = args.width, args.height
+    R = args.ring or (64 if args.path == "of" else 192)
     clip = SyntheticClip(W, H, seed=rank, noisy=args.noisy)
     order = pingpong(R)
     P = len(order)                 # frames per step (126 for R=64)
@@ -143,7 +148,7 @@ def main():
     of = args.path == "of"
     if of:   # the OF worker writes a mask plane instead of the red overlay
         ov = torch.empty((P, H, W), dtype=torch.uint8, device=dev)
-    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else 63), P))
+    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else 191), P))
 
     def make_worker(ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker

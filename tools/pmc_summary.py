@@ -1,9 +1,10 @@
 """Summarise two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into profiles/pmc_summary.json.
 
-    python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json> [workload]
+    python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json> [workload [frames_per_launch]]
 
-``workload`` (bench.py's config.workload of the profiled command) is recorded so
-bench.py only quotes the traffic for the workload it was measured on.
+``workload`` (bench.py's config.workload of the profiled command) and
+``frames_per_launch`` (its roofline.frames_per_launch) are recorded so bench.py
+only quotes the traffic for the workload and launch size it was measured on.
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md § HBM: on
 gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads;
@@ -41,6 +42,7 @@ def main():
                    "gfx950 FETCH_SIZE halves wide streaming reads (MI355X_MICROARCH.md), other access widths "
                    "uncalibrated; Infinity-Cache hits included",
            "workload": sys.argv[4] if len(sys.argv) > 4 else None,
+           "frames_per_launch": float(sys.argv[5]) if len(sys.argv) > 5 else None,
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, []), write.get(k, [])
