@@ -709,6 +709,7 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
         for (int u = 0; u < U; ++u) dst[u] = db[(size_t)min(t0 + u, a.n - 1) * NB + blk];   // clamped: unconditional
     };
     unsigned long long nstatic = 0;
+    const float dil0 = __builtin_fmaf(0.f, a.beta, a.gamma), dil1 = __builtin_fmaf(255.f, a.beta, a.gamma);
     auto frame = [&](int t, BT d) {
         uint32_t aor = 0;
 #pragma unroll
@@ -727,12 +728,14 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
                     uint32_t av = acv[i][q], nv = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const float dil = (float)(((dw >> (4 * q + j)) & 1u) ? 255 : 0);
+                        // fmaf(dil, beta, gamma) for dil in {0, 255}: one of two
+                        // uniform values; sat_u8(rint(t)): clamp (fmax/fmin send NaN
+                        // to 0 like the reference's saturate_cast) then an exact
+                        // integer -> byte conversion packed in place
                         const float tv = __builtin_fmaf((float)((av >> (8 * j)) & 255), a.alpha,
-                                                        __builtin_fmaf(dil, a.beta, a.gamma));
-                        const float rr = __builtin_rintf(tv);
-                        const uint32_t v = rr < 0.f ? 0u : (rr > 255.f ? 255u : (uint32_t)rr);
-                        nv |= v << (8 * j);
+                                                        ((dw >> (4 * q + j)) & 1u) ? dil1 : dil0);
+                        const float c = __builtin_fminf(__builtin_fmaxf(__builtin_rintf(tv), 0.f), 255.f);
+                        nv = __builtin_amdgcn_cvt_pk_u8_f32(c, (uint32_t)j, nv);
                     }
                     acv[i][q] = nv;
                     zero = zero && nv == 0;
