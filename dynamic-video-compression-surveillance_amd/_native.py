@@ -128,9 +128,10 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    path = os.environ.get("DVC_LIB_PATH") or LIB_PATH   # override: A/B runs of two builds
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the HIP path has no CPU fallback)")
     # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (same
     # SONAME). Loading torch first makes libdvc_hip.so bind to that instance, so
@@ -140,7 +141,7 @@ def lib() -> ctypes.CDLL:
         import torch  # noqa: F401
     except Exception:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, u8p = ctypes.c_void_p, ctypes.c_void_p
     L.dvc_abi_version.restype = ctypes.c_int
     L.dvc_last_error.restype = ctypes.c_char_p
