@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=("fd", "of"), default="fd",
                     help="fd: frame_differencing.py worker (headline); of: motion_compression_opt.py worker")
+    ap.add_argument("--block-size", type=int, default=4, help="FD block_size (fd:161; the __main__ variant uses 8)")
+    ap.add_argument("--kernel-size", type=int, default=7, help="FD dilation kernel_size (__main__: 10)")
+    ap.add_argument("--release-factor", type=float, default=0.5, help="FD release_factor (__main__: 0.3)")
     ap.add_argument("--batch", type=int, default=0, help="frames per device launch (max_batch; 0: 191 fd / 16 of)")
     ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
     args = ap.parse_args()
@@ -152,7 +155,9 @@ def main():
 
     def make_worker(ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
-        w = cls(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch)
+        kw = {} if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
+                                release_factor=args.release_factor)
+        w = cls(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch, **kw)
         w.prime(first)
         return w
 
@@ -209,6 +214,8 @@ def main():
         avg_ms = kms / max(kn, 1)
         res = f"{W}x{H}" if (W, H) != (1920, 1080) else "1080p"
         workload = f"{args.path}_{res}_single_feed_per_gpu"
+        if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
+            workload += f"_b{args.block_size}_k{args.kernel_size}_r{args.release_factor:g}"
         if of:   # kn counts level-0 k_flow launches (iterations per batch)
             kname = "k_flow"
             per_launch_frames = kframes * 2 / max(kn, 1)
