@@ -926,9 +926,11 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
                         uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
-    // chunks: ~5120 workgroups, at least 8 frames per chunk (1080p x 63: 7 chunks
-    // of 9 frames, measured best); DVC_FRONT_WGS / DVC_FRONT_MIN override for sweeps
-    static const int target = [] { const char* e = getenv("DVC_FRONT_WGS"); return e ? std::max(1, atoi(e)) : 5120; }();
+    // chunks: ~1280 workgroups, at least 8 frames per chunk (1080p x 191: 2
+    // chunks, measured best of 1..9 — each extra chunk re-reads a warm-up frame
+    // and adds workgroups competing with the contour filter); DVC_FRONT_WGS /
+    // DVC_FRONT_MIN override for sweeps
+    static const int target = [] { const char* e = getenv("DVC_FRONT_WGS"); return e ? std::max(1, atoi(e)) : 1280; }();
     int chunks = (target + tx * ty / 2) / (tx * ty);
     static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
     chunks = std::max(1, std::min(chunks, n / minf));
@@ -987,13 +989,13 @@ hipError_t launch_accumulate(const BackArgs& a, int block, hipStream_t s)
 hipError_t launch_out(const BackArgs& a, int block, hipStream_t s)
 {
     if (!a.overlay && !a.compressed) return hipSuccess;
-    // 64 workgroups per CU (16384 on MI355X, ~2 tiles each at 1080p x 63):
-    // measured best of 2k..34k beside the CCL chain; DVC_OUT_WGS overrides
+    // 128 workgroups per CU (32768 on MI355X): measured best of 8k..64k beside
+    // the CCL chain at 1080p x 191 (+1 % over 64/CU); DVC_OUT_WGS overrides
     static const int wgs = [] {
         if (const char* e = getenv("DVC_OUT_WGS")) return std::max(1, atoi(e));
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        return 64 * cus;
+        return 128 * cus;
     }();
     const int ntx = (a.g.W + 64 * block - 1) / (64 * block), nty = (a.g.H + 4 * block - 1) / (4 * block);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
