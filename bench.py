@@ -10,15 +10,16 @@ GPU (seed = rank), the full per-frame worker of frame_differencing.py:91-133 —
 gray, 5x5 blur, absdiff/threshold, contour-area filter, 7x7 dilate,
 accumulation, red overlay, static-block DCT quantisation, YCrCb round trip —
 with the GUI's default kwargs (windows.py:154). Frames are device-resident: R
-distinct synthetic frames (--ring; FD 192, OF 64) played ping-pong
+distinct synthetic frames (--ring; FD batch+1, OF 64) played ping-pong
 (0..R-1..1) so every consecutive pair is real motion, materialised as one
-contiguous (2R-2)-frame sequence (FD: 382 frames, 2.4 GB — far beyond the
-256 MB Infinity Cache); overlay and compressed outputs go to device buffers of
-the same length. A step = one pass over that sequence through
-dvc_fd_step_batch (launches of --batch frames, FD default 191: larger grids
-keep the latency-bound contour filter occupied and amortise the stage
-hand-offs — 63 frames measured 274 k Mpx/s, 191 310 k, 383 316 k; --per-frame:
-one dvc_fd_step per frame instead).
+contiguous (2R-2)-frame sequence (FD 1080p: 766 frames, 4.8 GB — far beyond
+the 256 MB Infinity Cache); overlay and compressed outputs go to device buffers
+of the same length. A step = one pass over that sequence through
+dvc_fd_step_batch (launches of --batch frames, FD default 383 at 1080p: larger
+grids keep the latency-bound contour filter occupied and amortise the stage
+hand-offs — interleaved sweeps: 127 → 276 k, 191 → 288 k, 255 → 291 k,
+383 → 298–307 k, 511 → 294 k Mpx/s; --per-frame: one dvc_fd_step per frame
+instead).
 
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
@@ -104,7 +105,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--ring", type=int, default=0, help="distinct frames (0: 192 fd / 64 of)")
+    ap.add_argument("--ring", type=int, default=0, help="distinct frames (0: batch+1 fd / 64 of)")
     ap.add_argument("--noisy", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -113,7 +114,8 @@ def main():
     ap.add_argument("--block-size", type=int, default=4, help="FD block_size (fd:161; the __main__ variant uses 8)")
     ap.add_argument("--kernel-size", type=int, default=7, help="FD dilation kernel_size (__main__: 10)")
     ap.add_argument("--release-factor", type=float, default=0.5, help="FD release_factor (__main__: 0.3)")
-    ap.add_argument("--batch", type=int, default=0, help="frames per device launch (max_batch; 0: 191 fd / 16 of)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per device launch (max_batch; 0: fd 383 at 1080p, scaled by pixels / of 16)")
     ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
     args = ap.parse_args()
 
@@ -133,7 +135,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     W, H = args.width, args.height
-    R = args.ring or (64 if args.path == "of" else 192)
+    # FD: 383-frame launches at 1080p (scaled by pixel count for larger frames)
+    fd_batch = max(31, min(383, 383 * 1920 * 1080 // (W * H)))
+    R = args.ring or (64 if args.path == "of" else fd_batch + 1)
     clip = SyntheticClip(W, H, seed=rank, noisy=args.noisy)
     order = pingpong(R)
     P = len(order)                 # frames per step (126 for R=64)
@@ -151,7 +155,7 @@ def main():
     of = args.path == "of"
     if of:   # the OF worker writes a mask plane instead of the red overlay
         ov = torch.empty((P, H, W), dtype=torch.uint8, device=dev)
-    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else 191), P))
+    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else fd_batch), P))
 
     def make_worker(ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
