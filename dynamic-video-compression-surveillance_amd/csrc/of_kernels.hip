@@ -376,40 +376,46 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
             const float* r0 = r0v[u];
             const float* p = pq[u];
             const float* q = pq[u] + 10;
-            float r2, r3, r4, r5, r6;
+            // channel pairs (r2, r3), (r4, r5) as packed f32x2 (v_pk_mul/add_f32,
+            // each lane the same mul-then-add sequence as the scalar form), r6 scalar
+            f32x2 R23, R45;
+            float r6;
+            const f32x2 R0_01 = {r0[0], r0[1]}, R0_23 = {r0[2], r0[3]};
             if (inb[u]) {
                 const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
-                r2 = a00 * p[0] + a01 * p[5] + a10 * q[0] + a11 * q[5];
-                r3 = a00 * p[1] + a01 * p[6] + a10 * q[1] + a11 * q[6];
-                r4 = a00 * p[2] + a01 * p[7] + a10 * q[2] + a11 * q[7];
-                r5 = a00 * p[3] + a01 * p[8] + a10 * q[3] + a11 * q[8];
+                const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
+                const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
+                const f32x2 Q01 = {q[0], q[1]}, Q23 = {q[2], q[3]}, Q56 = {q[5], q[6]}, Q78 = {q[7], q[8]};
+                R23 = A00 * P01 + A01 * P56 + A10 * Q01 + A11 * Q56;
+                R45 = A00 * P23 + A01 * P78 + A10 * Q23 + A11 * Q78;
                 r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
-                r4 = (r0[2] + r4) * 0.5f;
-                r5 = (r0[3] + r5) * 0.5f;
+                R45 = (R0_23 + R45) * (f32x2)0.5f;
                 r6 = (r0[4] + r6) * 0.25f;
             } else {
-                r2 = r3 = 0.f;
-                r4 = r0[2];
-                r5 = r0[3];
+                R23 = (f32x2)0.f;
+                R45 = R0_23;
                 r6 = r0[4] * 0.5f;
             }
-            r2 = (r0[0] - r2) * 0.5f;
-            r3 = (r0[1] - r3) * 0.5f;
-            r2 += r4 * dy + r6 * dx;
-            r3 += r6 * dy + r5 * dx;
+            R23 = (R0_01 - R23) * (f32x2)0.5f;
+            // r2 += r4 dy + r6 dx;  r3 += r6 dy + r5 dx
+            R23 = R23 + ((f32x2){R45.x, r6} * (f32x2)dy + (f32x2){r6, R45.y} * (f32x2)dx);
             if constexpr (!INT) {
                 if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
                     const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
                                         (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
-                    r2 *= scale; r3 *= scale; r4 *= scale; r5 *= scale; r6 *= scale;
+                    R23 = R23 * (f32x2)scale;
+                    R45 = R45 * (f32x2)scale;
+                    r6 *= scale;
                 }
             }
             float* M = sM + (size_t)idx[u] * 5;
-            M[0] = r4 * r4 + r6 * r6;
-            M[1] = (r4 + r5) * r6;
-            M[2] = r5 * r5 + r6 * r6;
-            M[3] = r4 * r2 + r6 * r3;
-            M[4] = r6 * r2 + r5 * r3;
+            const f32x2 G = R45 * R45 + (f32x2)(r6 * r6);                                   // (M0, M2)
+            const f32x2 Hh = (f32x2){R45.x, r6} * (f32x2)R23.x + (f32x2){r6, R45.y} * (f32x2)R23.y;   // (M3, M4)
+            M[0] = G.x;
+            M[1] = (R45.x + R45.y) * r6;
+            M[2] = G.y;
+            M[3] = Hh.x;
+            M[4] = Hh.y;
         }
     }
     __syncthreads();
