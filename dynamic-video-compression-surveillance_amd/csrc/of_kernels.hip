@@ -54,10 +54,11 @@ __device__ __forceinline__ int ring(long long a, int n)
 // ------------------------------------------------- polynomial expansion -----
 // Steps C and D of FarnebackPolyExp (oc_poly_exp) for one tile whose smoothed
 // level image I is in LDS at rows [y0-PN, y0+PT_H-1+PN], cols [x0-PN, ...]
-// (in-image entries only). sv: PT_H x (PT_W+2PN) x 3 floats.
-template <int PN>
-__device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0, int y0, int w, int h,
-                          float* __restrict__ R)
+// (in-image entries only). sv: PT_H x (PT_W+2PN) x 3 floats. INT: the tile and
+// its PN halo lie inside the image (no clamping; LDS offsets are constants).
+template <int PN, bool INT = false>
+__device__ __forceinline__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0, int y0, int w,
+                                          int h, float* __restrict__ R)
 {
     constexpr int IW = PT_W + 2 * PN;
     const int tid = threadIdx.x;
@@ -65,14 +66,14 @@ __device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0
     for (int idx = tid; idx < PT_H * IW; idx += 256) {
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 + i, x = x0 - PN + j;
-        if (y >= h || x < 0 || x >= w) continue;
+        if (!INT && (y >= h || x < 0 || x >= w)) continue;
         const int li = i + PN;
         float r0 = sI[li * IW + j] * pc.g[PN];
         float r1 = 0.f, r2 = 0.f;
 #pragma unroll
         for (int k = 1; k <= PN; ++k) {
             const float g0 = pc.g[PN + k], g1 = pc.xg[PN + k], g2 = pc.xxg[PN + k];
-            const int ya = max(y - k, 0) - (y0 - PN), yb = min(y + k, h - 1) - (y0 - PN);
+            const int ya = INT ? li - k : max(y - k, 0) - (y0 - PN), yb = INT ? li + k : min(y + k, h - 1) - (y0 - PN);
             const float a = sI[ya * IW + j], b = sI[yb * IW + j];
             const float p = a + b;
             const float t0 = r0 + g0 * p;
@@ -93,15 +94,15 @@ __device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0
     for (int idx = tid; idx < PT_H * PT_W; idx += 256) {
         const int i = idx / PT_W, jx = idx - i * PT_W;
         const int y = y0 + i, x = x0 + jx;
-        if (y >= h || x >= w) continue;
+        if (!INT && (y >= h || x >= w)) continue;
         const float* c = sv + (i * IW + jx + PN) * 3;
         const float gc = pc.g[PN];
         double b1 = (double)(c[0] * gc), b2 = 0, b3 = (double)(c[1] * gc), b4 = 0;
         double b5 = (double)(c[2] * gc), b6 = 0;
 #pragma unroll
         for (int k = 1; k <= PN; ++k) {
-            const float* P = sv + (i * IW + (min(x + k, w - 1) - (x0 - PN))) * 3;
-            const float* M = sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
+            const float* P = INT ? c + 3 * k : sv + (i * IW + (min(x + k, w - 1) - (x0 - PN))) * 3;
+            const float* M = INT ? c - 3 * k : sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
             const float gk = pc.g[PN + k], xgk = pc.xg[PN + k];
             const double tg = (double)(P[0] + M[0]);
             b1 += tg * (double)gk;
@@ -111,7 +112,7 @@ __device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0
             b6 += (double)((P[1] - M[1]) * xgk);
             b5 += (double)((P[2] + M[2]) * gk);
         }
-        float* d = R + ((size_t)y * w + x) * 5;
+        float* d = R + 5u * (uint32_t)(y * w + x);
         d[1] = (float)(b2 * pc.ig11);
         d[0] = (float)(b3 * pc.ig11);
         d[3] = (float)(b1 * pc.ig03 + b4 * pc.ig33);
@@ -127,19 +128,16 @@ __device__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0
 // (PN+1) halo, the level-0 smoothing (GaussianBlur 3x3, sigma 0 -> taps
 // (0.25, 0.5, 0.25), BORDER_REFLECT_101) over tile + PN halo, then the
 // polynomial expansion. blockIdx.z = frame of the batch.
-template <int PN>
-__global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* __restrict__ gray_out,
-                                                   const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
-                                                   long long a0)
+template <int PN, bool INT>
+__device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, uint8_t* __restrict__ gray_out,
+                                            const uint8_t* __restrict__ bgr, int pitch, size_t fstride, long long a0,
+                                            float* sg, float* sI, float* sv)
 {
     // gray tile: rows y0-HG .., columns from x0-GX in whole 4-px quads (GX = 8 >= HG
     // keeps each quad's 12 BGR bytes 4-byte aligned: x0 % 64 == 0, pitch % 4 == 0)
     constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG, NQ = GW / 4;
     constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
     static_assert(HG <= GX, "halo wider than the quad pad");
-    __shared__ __attribute__((aligned(16))) float sg[GH * GW];
-    __shared__ float sI[IH * IW];
-    __shared__ float sv[PT_H * IW * 3];
     const int tid = threadIdx.x, t = blockIdx.z;
     const int W = g.W, H = g.H;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
@@ -148,7 +146,7 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
     for (int idx = tid; idx < GH * NQ; idx += 256) {
         const int i = idx / NQ, q = idx - i * NQ;
         const int y = y0 - HG + i, px = x0 - GX + 4 * q;
-        if (y < 0 || y >= H || px < 0 || px >= W) continue;   // W % 8 == 0: quads are whole
+        if (!INT && (y < 0 || y >= H || px < 0 || px >= W)) continue;   // W % 8 == 0: quads are whole
         const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)y * pitch + 3 * px);
         const uint32_t gq = gray4_dot(v.x, v.y, v.z);   // of:71 BGR2GRAY of 4 px
         *reinterpret_cast<float4*>(sg + i * GW + 4 * q) =
@@ -162,10 +160,11 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
     for (int idx = tid; idx < IH * IW; idx += 256) {
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 - PN + i, x = x0 - PN + j;
-        if (y < 0 || y >= H || x < 0 || x >= W) continue;
-        const int xl = reflect1(x - 1, W) - (x0 - GX), xc = x - (x0 - GX), xr = reflect1(x + 1, W) - (x0 - GX);
+        if (!INT && (y < 0 || y >= H || x < 0 || x >= W)) continue;
+        const int xc = x - (x0 - GX);
+        const int xl = INT ? xc - 1 : reflect1(x - 1, W) - (x0 - GX), xr = INT ? xc + 1 : reflect1(x + 1, W) - (x0 - GX);
         float hv[3];
-        const int ys[3] = {reflect1(y - 1, H), y, reflect1(y + 1, H)};
+        const int ys[3] = {INT ? y - 1 : reflect1(y - 1, H), y, INT ? y + 1 : reflect1(y + 1, H)};
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             const float* s = sg + (ys[q] - (y0 - HG)) * GW;
@@ -179,7 +178,25 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
     }
     __syncthreads();
     float* R = lv.R + (size_t)ring(a0 + t, g.RS) * W * H * 5;
-    poly_tile<PN>(sI, sv, g.pc, x0, y0, W, H, R);
+    poly_tile<PN, INT>(sI, sv, g.pc, x0, y0, W, H, R);
+}
+
+// Interior tiles (the tile with its GX-px quad pad and HG-row halo inside the
+// frame) take the unclamped form: the same arithmetic on the same values.
+template <int PN>
+__global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* __restrict__ gray_out,
+                                                   const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
+                                                   long long a0)
+{
+    constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG;
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    __shared__ __attribute__((aligned(16))) float sg[GH * GW];
+    __shared__ float sI[IH * IW];
+    __shared__ float sv[PT_H * IW * 3];
+    const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
+    const bool interior = x0 >= GX && x0 + PT_W + GX <= g.W && y0 >= HG && y0 + PT_H + HG <= g.H;   // uniform
+    if (interior) front0_tile<PN, true>(g, lv, gray_out, bgr, pitch, fstride, a0, sg, sI, sv);
+    else front0_tile<PN, false>(g, lv, gray_out, bgr, pitch, fstride, a0, sg, sI, sv);
 }
 
 // ----------------------------------------------------------- level k > 0 ----
