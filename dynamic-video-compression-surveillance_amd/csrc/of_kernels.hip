@@ -218,7 +218,11 @@ __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t
         const LinTap tp = lv.xt[j >> 1];
         const int c = (j & 1) ? tp.s1 : tp.s0;
         float acc = lv.kf[r] * (float)s[c];
-        for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
+        if (c >= r && c + r < W)   // taps inside the row: reflect101 is the identity
+            for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[c - i] + (float)s[c + i]);
+        else
+            for (int i = 1; i <= r; ++i)
+                acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
         out[j] = acc;
     }
 }
@@ -235,19 +239,23 @@ __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
     const int row = (yy & 1) ? ty.s1 : ty.s0;
     const float* T = lv.tmpc + (size_t)t * H * n2 + j;
     float acc = lv.kf[r] * T[(size_t)row * n2];
-    for (int i = 1; i <= r; ++i)
-        acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
+    if (row >= r && row + r < H) {   // uniform per workgroup (one row)
+        const float* C = T + (uint32_t)(row * n2);
+        for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (C[-(int)(i * n2)] + C[i * n2]);
+    } else {
+        for (int i = 1; i <= r; ++i)
+            acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
+    }
     lv.vtmp[((size_t)t * 2 * lv.h + yy) * n2 + j] = acc;
 }
 
 // The INTER_LINEAR combination (oc_resize_linear_f32) over tile + PN halo from
-// vtmp, then the polynomial expansion of the level image.
-template <int PN>
-__global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long a0)
+// vtmp, then the polynomial expansion of the level image. INT: tile + halo
+// inside the level image (no skipped positions, no clamped taps).
+template <int PN, bool INT>
+__device__ __forceinline__ void pyr_poly_tile(const OfGeom& g, const Level& lv, long long a0, float* sI, float* sv)
 {
     constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
-    __shared__ float sI[IH * IW];
-    __shared__ float sv[PT_H * IW * 3];
     const int tid = threadIdx.x, t = blockIdx.z;
     const int w = lv.w, h = lv.h, n2 = 2 * w;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
@@ -255,9 +263,9 @@ __global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long 
     for (int idx = tid; idx < IH * IW; idx += 256) {
         const int i = idx / IW, j = idx - i * IW;
         const int y = y0 - PN + i, x = x0 - PN + j;
-        if (y < 0 || y >= h || x < 0 || x >= w) continue;
+        if (!INT && (y < 0 || y >= h || x < 0 || x >= w)) continue;
         const LinTap ty = lv.yt[y], tx = lv.xt[x];
-        const float* v0 = V + (size_t)(2 * y) * n2 + 2 * x;
+        const float* v0 = V + (uint32_t)(2 * y * n2 + 2 * x);
         const float* v1 = v0 + n2;
         const float t0 = v0[0] * tx.w0 + v0[1] * tx.w1;
         const float t1 = v1[0] * tx.w0 + v1[1] * tx.w1;
@@ -265,7 +273,20 @@ __global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long 
     }
     __syncthreads();
     float* R = lv.R + (size_t)ring(a0 + t, g.RS) * w * h * 5;
-    poly_tile<PN>(sI, sv, g.pc, x0, y0, w, h, R);
+    poly_tile<PN, INT>(sI, sv, g.pc, x0, y0, w, h, R);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long a0)
+{
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    __shared__ float sI[IH * IW];
+    __shared__ float sv[PT_H * IW * 3];
+    const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
+    if (x0 >= PN && x0 + PT_W + PN <= lv.w && y0 >= PN && y0 + PT_H + PN <= lv.h)
+        pyr_poly_tile<PN, true>(g, lv, a0, sI, sv);
+    else
+        pyr_poly_tile<PN, false>(g, lv, a0, sI, sv);
 }
 
 // -------------------------------------------------------------------- flow --
