@@ -24,11 +24,12 @@ DVC_OK = 0
 DVC_FLAG_DEVICE_PTRS = 0x1
 DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
+DVC_FLAG_JOIN_STREAM = 0x8
 
 PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
 OF_PLANE_RAW, OF_PLANE_SMOOTH, OF_PLANE_MORPH, OF_PLANE_RECT, OF_PLANE_GRAY = range(5)
 
-# every symbol include/dvc.h declares (checked by tests/test_abi.py)
+# every symbol include/dvc.h declares (checked by tests/test_host.py::test_abi_exports_every_declared_symbol)
 EXPORTS = [
     "dvc_abi_version", "dvc_last_error", "dvc_device_count", "dvc_fd_create", "dvc_fd_prime",
     "dvc_fd_step", "dvc_fd_sync", "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime",

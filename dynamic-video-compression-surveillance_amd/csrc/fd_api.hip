@@ -121,8 +121,10 @@ constexpr int NSLOT = 3;
 struct dvc_fd {
     dvc_fd_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;  // prime + contour filter; the caller's stream if given
-    bool own_stream = false;
+    hipStream_t stream = nullptr;  // prime + contour filter (internal)
+    hipStream_t user = nullptr;    // the caller's stream (create's hip_stream; NULL = legacy default)
+    bool has_user = false;         // join `user` (hip_stream given, or DVC_FLAG_JOIN_STREAM)
+    hipEvent_t ev_user = nullptr, ev_join_out = nullptr, ev_join_acc = nullptr;
     hipStream_t s_front = nullptr;       // blur/threshold front (previous-gray recurrence)
     hipStream_t s_acc = nullptr;         // dilate + accumulate (accumulated-mask recurrence)
     hipStream_t s_out = nullptr;         // overlay + compressed frames
@@ -169,15 +171,40 @@ static void free_all(dvc_fd* h)
     for (void* p : pin)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
-    for (hipStream_t st : {h->s_front, h->s_acc, h->s_out})
+    for (hipEvent_t e : {h->ev_user, h->ev_join_out, h->ev_join_acc})
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {h->s_front, h->s_acc, h->s_out, h->stream})
         if (st) (void)hipStreamDestroy(st);
-    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
 }
 
 template <typename T>
 static hipError_t dalloc(T** p, size_t bytes)
 {
     return hipMalloc(reinterpret_cast<void**>(p), bytes ? bytes : 16);
+}
+
+// The caller's stream (if any) -> every internal stream: work the caller queued
+// before this call (e.g. the copy that produced the frames, or reads of the
+// previous outputs) happens before the call's kernels.
+static hipError_t wait_user(dvc_fd* h)
+{
+    if (!h->has_user) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_user, h->user);
+    for (hipStream_t st : {h->stream, h->s_front, h->s_acc, h->s_out})
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ev_user, 0);
+    return e;
+}
+
+// Internal streams -> the caller's stream: work the caller queues after this
+// call sees its outputs (overlay/compressed on s_out, acc_out on s_acc).
+static hipError_t join_user(dvc_fd* h)
+{
+    if (!h->has_user) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_join_out, h->s_out);
+    if (e == hipSuccess) e = hipEventRecord(h->ev_join_acc, h->s_acc);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->user, h->ev_join_out, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->user, h->ev_join_acc, 0);
+    return e;
 }
 
 static hipError_t sync_all(dvc_fd* h)
@@ -247,18 +274,20 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     };
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bad(e, "hipSetDevice");
-    if (hip_stream) h->stream = (hipStream_t)hip_stream;
-    // four streams in all — the handle's (contour filter), front, accumulate,
-    // output — within the default 4 hardware queues (a queue shared by two
-    // stages serialises them); priorities: the latency-bound contour filter and
-    // accumulate chains high, the VALU-bound front low
+    h->user = (hipStream_t)hip_stream;
+    h->has_user = hip_stream != nullptr || (p.flags & DVC_FLAG_JOIN_STREAM);
+    // four internal streams — contour filter, front, accumulate, output —
+    // within the default 4 hardware queues (a queue shared by two stages
+    // serialises them); priorities: the latency-bound contour filter and
+    // accumulate chains high, the VALU-bound front low. The caller's stream (if
+    // any) is only joined: each call waits for the work queued on it before the
+    // call, and work queued on it after the call waits for the call's outputs.
     int plo = 0, phi = 0;
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
     auto mk = [](hipStream_t* st, int prio) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio); };
-    if (!hip_stream) {
-        if ((e = mk(&h->stream, phi)) != hipSuccess) return bad(e, "hipStreamCreate");
-        h->own_stream = true;
-    }
+    if ((e = mk(&h->stream, phi)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (hipEvent_t* ev : {&h->ev_user, &h->ev_join_out, &h->ev_join_acc})
+        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     for (auto sp : {std::make_pair(&h->s_front, plo), std::make_pair(&h->s_acc, phi), std::make_pair(&h->s_out, 0)})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
@@ -320,6 +349,7 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
         HIP_OK(dalloc(&h->gtmp, N));
     }
     HIP_OK(sync_all(h));  // no batch of a previous run may still be in flight
+    HIP_OK(wait_user(h));
     const uint8_t* d = bgr;
     int dp = (int)pitch;
     if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
@@ -439,6 +469,7 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
     if (n > 1 && (overlay || compressed) && (ostride < 3 * N || ostride % 4))
         return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
+    HIP_OK(wait_user(h));
     const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
     for (int f0 = 0; f0 < n; f0 += h->max_batch) {
         const int m = std::min(h->max_batch, n - f0);
@@ -473,6 +504,7 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
             std::memcpy(acc_out, h->h_acc, N);
         }
     }
+    HIP_OK(join_user(h));
     return DVC_OK;
 }
 

@@ -123,8 +123,10 @@ struct OfSlot {
 struct dvc_of {
     dvc_of_params p{};
     int device = 0;
-    hipStream_t stream = nullptr;  // prime + pyramid stage (s_pyr); the caller's stream if given
-    bool own_stream = false;
+    hipStream_t stream = nullptr;  // prime + pyramid stage (s_pyr), internal
+    hipStream_t user = nullptr;    // the caller's stream (create's hip_stream; NULL = legacy default)
+    bool has_user = false;         // join `user` (hip_stream given, or DVC_FLAG_JOIN_STREAM)
+    hipEvent_t ev_user = nullptr, ev_join = nullptr;
     // batch i: s_pyr [wait flow(i-2)] pyramid(i); s_flow [wait pyramid(i),
     // mask(i-2)] flow(i); s_mask [wait flow(i)] vote/morphology/rects + out(i)
     hipStream_t s_pyr = nullptr, s_flow = nullptr, s_mask = nullptr;
@@ -157,9 +159,29 @@ static void of_free(dvc_of* h)
     for (OfSlot& sl : h->slot)
         for (hipEvent_t e : {sl.ev_pyr, sl.ev_flow, sl.ev_mask})
             if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {h->s_flow, h->s_mask})
+    for (hipEvent_t e : {h->ev_user, h->ev_join})
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t st : {h->s_flow, h->s_mask, h->stream})
         if (st) (void)hipStreamDestroy(st);
-    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+// The caller's stream (if any) -> the internal streams, before a call's work;
+// the internal streams -> the caller's stream after it (outputs on s_mask).
+static hipError_t of_wait_user(dvc_of* h)
+{
+    if (!h->has_user) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_user, h->user);
+    for (hipStream_t st : {h->stream, h->s_flow, h->s_mask})
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, h->ev_user, 0);
+    return e;
+}
+
+static hipError_t of_join_user(dvc_of* h)
+{
+    if (!h->has_user) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_join, h->s_mask);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->user, h->ev_join, 0);
+    return e;
 }
 
 static hipError_t of_sync_all(dvc_of* h)
@@ -251,17 +273,17 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     };
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return bad(e, "hipSetDevice");
-    if (hip_stream) h->stream = (hipStream_t)hip_stream;
-    // three streams in all (the handle's own carries the pyramid): within the
-    // default 4 hardware queues beside the framework's stream, so no two stages
-    // share a queue (a shared queue serialises them)
+    h->user = (hipStream_t)hip_stream;
+    h->has_user = hip_stream != nullptr || (p.flags & DVC_FLAG_JOIN_STREAM);
+    // three internal streams (pyramid, flow, mask/output): within the default 4
+    // hardware queues beside the framework's stream, so no two stages share a
+    // queue (a shared queue serialises them); the caller's stream is only joined
     // equal priorities: the flow and pyramid stages alternate as the critical
     // chain (interleaved sweep after the packed M phase: equal 16.15 k, flow +
     // mask high / pyramid low 15.88 k Mpx/s)
-    if (!hip_stream) {
-        if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-        h->own_stream = true;
-    }
+    if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (hipEvent_t* ev : {&h->ev_user, &h->ev_join})
+        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     h->s_pyr = h->stream;
     for (hipStream_t* st : {&h->s_flow, &h->s_mask})
         if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
@@ -371,6 +393,7 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_sync_all(h));   // no batch of a previous run may still be in flight
+    HIP_OK(of_wait_user(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
     const uint8_t* d = bgr;
     int dp = (int)pitch;
@@ -462,6 +485,7 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
     if (n > 1 && compressed && (ostride < 3 * N || ostride % 4))
         return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
+    HIP_OK(of_wait_user(h));
     const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
     for (int f0 = 0; f0 < n; f0 += h->max_batch) {
         const int m = std::min(h->max_batch, n - f0);
@@ -487,6 +511,7 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
             if (cp) std::memcpy(cp + (size_t)t * ostride, h->h_cp + (size_t)t * 3 * N, 3 * N);
         }
     }
+    HIP_OK(of_join_user(h));
     return DVC_OK;
 }
 

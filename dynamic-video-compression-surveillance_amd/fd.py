@@ -15,6 +15,7 @@ import math
 
 import numpy as np
 
+from . import _buffers as B
 from . import _native as N
 
 
@@ -47,44 +48,43 @@ def derive_params(width: int, height: int, block_size: int = 4, motion_threshold
     return p
 
 
-def _addr(x) -> int:
-    if isinstance(x, int):
-        return x
-    if hasattr(x, "data_ptr"):
-        return int(x.data_ptr())
-    raise TypeError(f"device mode needs a device tensor or an address, got {type(x)!r}")
-
-
 class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
                  device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
                  max_batch: int = 1, **kwargs):
         """``max_batch``: frames one device launch covers in :meth:`step_batch`
-        (the contour-filter scratch is sized for 2 x max_batch frames)."""
+        (the contour-filter scratch is sized for NSLOT = 3 batches of max_batch
+        frames in flight, fd_api.hip). ``stream``: the caller's HIP stream
+        (``torch.cuda.Stream.cuda_stream``), joined as dvc_fd_create documents."""
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
-            | (N.DVC_FLAG_KTIMING if ktiming else 0)
+            | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0)
         self.params = derive_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
+        self.device = int(device)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
         h = ctypes.c_void_p()
         s = ctypes.c_void_p(int(stream)) if stream is not None else None
-        N.check(self._lib.dvc_fd_create(ctypes.byref(self.params), int(device), s, ctypes.byref(h)))
+        N.check(self._lib.dvc_fd_create(ctypes.byref(self.params), self.device, s, ctypes.byref(h)))
         self._h = h
 
     # -------------------------------------------------------------- frames --
-    def _host_frame(self, frame: np.ndarray) -> np.ndarray:
-        if not isinstance(frame, np.ndarray) or frame.dtype != np.uint8 or frame.shape != (self.H, self.W, 3):
-            raise ValueError(f"expected uint8 BGR frame of shape {(self.H, self.W, 3)}")
-        return np.ascontiguousarray(frame)
+    @property
+    def _fshape(self):
+        return (self.H, self.W, 3)
+
+    def _dev(self, x, name, n=None, batched=False, tail=None):
+        addr, m = B.device_buf(x, tail or self._fshape, self.device, name, n=n, batched=batched)
+        return addr, m
 
     def prime(self, frame) -> None:
         """fd:67-81: previous gray := GaussianBlur(gray(frame), 25x25, 30); acc := 0."""
         if self.device_ptrs:
-            N.check(self._lib.dvc_fd_prime(self._h, _addr(frame), 3 * self.W))
+            addr, _ = self._dev(frame, "frame")
+            N.check(self._lib.dvc_fd_prime(self._h, addr, 3 * self.W))
         else:
-            f = self._host_frame(frame)
+            f = B.host_in(frame, self._fshape, "frame")
             N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, 3 * self.W))
 
     def step(self, frame, overlay=None, compressed=None, acc=None, want=("overlay", "compressed")):
@@ -95,16 +95,16 @@ class FDWorker:
         into the given device buffers (None = not produced) and returns None.
         """
         if self.device_ptrs:
-            N.check(self._lib.dvc_fd_step(self._h, _addr(frame), 3 * self.W,
-                                          _addr(overlay) if overlay is not None else None,
-                                          _addr(compressed) if compressed is not None else None,
-                                          _addr(acc) if acc is not None else None))
+            addr, _ = self._dev(frame, "frame")
+            ov = self._dev(overlay, "overlay")[0] if overlay is not None else None
+            cp = self._dev(compressed, "compressed")[0] if compressed is not None else None
+            ac = self._dev(acc, "acc", tail=(self.H, self.W))[0] if acc is not None else None
+            N.check(self._lib.dvc_fd_step(self._h, addr, 3 * self.W, ov, cp, ac))
             return None
-        f = self._host_frame(frame)
-        if overlay is None and "overlay" in want:
-            overlay = np.empty_like(f)
-        if compressed is None and "compressed" in want:
-            compressed = np.empty_like(f)
+        f = B.host_in(frame, self._fshape, "frame")
+        overlay = B.host_out(overlay, self._fshape, "overlay", "overlay" in want)
+        compressed = B.host_out(compressed, self._fshape, "compressed", "compressed" in want)
+        acc = B.host_out(acc, (self.H, self.W), "acc", False)
         N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, 3 * self.W,
                                       overlay.ctypes.data if overlay is not None else None,
                                       compressed.ctypes.data if compressed is not None else None,
@@ -117,31 +117,24 @@ class FDWorker:
         Host mode: ``frames`` is an (n, H, W, 3) uint8 array; returns
         ``(overlay, compressed)`` arrays of the same shape (allocated if not
         given; a name missing from ``want`` is None). Device mode: ``frames``,
-        ``overlay``, ``compressed`` are (n, H, W, 3) uint8 device tensors or
-        ``(address, n)`` tuples of contiguous frames; asynchronous, returns None.
+        ``overlay``, ``compressed`` are (n, H, W, 3) uint8 CUDA tensors on the
+        handle's device (outputs may hold more frames), or explicit
+        ``(address, n)`` tuples of dense frames; asynchronous, returns None.
         """
         fs = 3 * self.W * self.H
         if self.device_ptrs:
-            if isinstance(frames, tuple):
-                addr, n = int(frames[0]), int(frames[1])
-            else:
-                n = int(frames.shape[0])
-                addr = _addr(frames)
-            ov = _addr(overlay[0] if isinstance(overlay, tuple) else overlay) if overlay is not None else None
-            cp = _addr(compressed[0] if isinstance(compressed, tuple) else compressed) if compressed is not None else None
+            addr, n = self._dev(frames, "frames", batched=True)
+            ov = self._dev(overlay, "overlay", n=n, batched=True)[0] if overlay is not None else None
+            cp = self._dev(compressed, "compressed", n=n, batched=True)[0] if compressed is not None else None
             N.check(self._lib.dvc_fd_step_batch(self._h, addr, 3 * self.W, fs, n, ov, cp, fs))
             return None
-        f = np.ascontiguousarray(frames)
-        if f.dtype != np.uint8 or f.ndim != 4 or f.shape[1:] != (self.H, self.W, 3):
-            raise ValueError(f"expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
-        if overlay is None and "overlay" in want:
-            overlay = np.empty_like(f)
-        if compressed is None and "compressed" in want:
-            compressed = np.empty_like(f)
-        for o in (overlay, compressed):
-            if o is not None and (o.shape != f.shape or o.dtype != np.uint8 or not o.flags.c_contiguous):
-                raise ValueError("output arrays must be contiguous uint8 of the frames' shape")
-        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, int(f.shape[0]),
+        if not isinstance(frames, np.ndarray) or frames.ndim != 4:
+            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
+        n = int(frames.shape[0])
+        f = B.host_in(frames, (n,) + self._fshape, "frames")
+        overlay = B.host_out(overlay, f.shape, "overlay", "overlay" in want)
+        compressed = B.host_out(compressed, f.shape, "compressed", "compressed" in want)
+        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, n,
                                             overlay.ctypes.data if overlay is not None else None,
                                             compressed.ctypes.data if compressed is not None else None, fs))
         return overlay, compressed

@@ -10,8 +10,11 @@ CPU), plus the max-over-ranks wall time.
 """
 from __future__ import annotations
 
+import hashlib
 import os
-from typing import Iterable, Sequence
+from typing import Callable, Iterable, Sequence
+
+import numpy as np
 
 STAT_KEYS = ("frames", "motion_px", "components", "static_blocks")
 
@@ -68,3 +71,61 @@ def process_feeds(video_paths: Iterable[str], output_dir: str, technique: str = 
     for p in mine:
         run(p, output_dir, **kwargs)
     return mine
+
+
+def run_feed(source: str, make_worker: Callable, read_ahead: int = 16) -> dict:
+    """Stream one feed through a per-frame worker and return its counters.
+
+    ``make_worker(width, height)`` returns an object with ``prime(frame)``,
+    ``step_batch(frames) -> (overlay, compressed)``, ``stats()`` and
+    ``close()`` — an :class:`~dvc_amd.fd.FDWorker` in the product (frames
+    ``read_ahead`` at a time through one ``dvc_fd_step_batch`` call). Frame 0
+    primes the feed (fd:67-77); every later frame is one iteration of fd:85-138.
+    The returned dict holds the worker's counters plus ``digest``, a SHA-256
+    over every output frame in order, so a feed's results can be compared
+    across ranks and runs without shipping the frames.
+    """
+    from . import video_io
+    cap = video_io.open_source(source)
+    if not cap.isOpened():
+        raise FileNotFoundError(source)
+    W = int(cap.get(video_io.CAP_PROP_FRAME_WIDTH))
+    H = int(cap.get(video_io.CAP_PROP_FRAME_HEIGHT))
+    ok, first = cap.read()
+    if not ok:
+        raise ValueError(f"{source}: no frames")
+    w = make_worker(W, H)
+    digest = hashlib.sha256()
+    try:
+        w.prime(first)
+        buf = []
+        while True:
+            ok, f = cap.read()
+            if ok:
+                buf.append(f)
+            if buf and (not ok or len(buf) == read_ahead):
+                ov, cp = w.step_batch(np.stack(buf))
+                for t in range(len(buf)):
+                    digest.update(np.ascontiguousarray(ov[t]).tobytes())
+                    digest.update(np.ascontiguousarray(cp[t]).tobytes())
+                buf = []
+            if not ok:
+                break
+        st = dict(w.stats())
+    finally:
+        cap.release()
+        w.close()
+    st["digest"] = digest.hexdigest()
+    return st
+
+
+def run_feeds(sources: Sequence[str], make_worker: Callable, read_ahead: int = 16, device=None):
+    """This rank's shard of ``sources`` through :func:`run_feed`, then the one
+    end-of-run collective (:func:`aggregate`). Returns (per-feed results of this
+    rank, aggregate over all ranks)."""
+    import time
+    rank, world, _ = dist_env()
+    t0 = time.perf_counter()
+    mine = {src: run_feed(src, make_worker, read_ahead) for src in shard(list(sources), rank, world)}
+    total = {k: sum(r[k] for r in mine.values()) for k in STAT_KEYS}
+    return mine, aggregate(total, elapsed_s=time.perf_counter() - t0, device=device)

@@ -16,8 +16,8 @@ import ctypes
 
 import numpy as np
 
+from . import _buffers as B
 from . import _native as N
-from .fd import _addr
 
 
 def derive_of_params(width: int, height: int, flow_threshold: float = 0.5, alpha_fraction: float = 0.2,
@@ -42,31 +42,31 @@ class OFWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None, device_ptrs: bool = False,
                  keep_planes: bool = False, ktiming: bool = False, max_batch: int = 1, **kwargs):
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
-            | (N.DVC_FLAG_KTIMING if ktiming else 0)
+            | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0)
         self.params = derive_of_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
+        self.device = int(device)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
         h = ctypes.c_void_p()
         s = ctypes.c_void_p(int(stream)) if stream is not None else None
-        N.check(self._lib.dvc_of_create(ctypes.byref(self.params), int(device), s, ctypes.byref(h)))
+        N.check(self._lib.dvc_of_create(ctypes.byref(self.params), self.device, s, ctypes.byref(h)))
         self._h = h
 
-    def _host_frames(self, frames: np.ndarray, batched: bool) -> np.ndarray:
-        shape = (self.H, self.W, 3)
-        f = np.ascontiguousarray(frames)
-        ok = f.dtype == np.uint8 and (f.shape[1:] == shape and f.ndim == 4 if batched else f.shape == shape)
-        if not ok:
-            raise ValueError(f"expected uint8 BGR frame(s) of shape {shape}")
-        return f
+    @property
+    def _fshape(self):
+        return (self.H, self.W, 3)
+
+    def _dev(self, x, name, tail, n=None, batched=False) -> int:
+        return B.device_buf(x, tail, self.device, name, n=n, batched=batched)
 
     def prime(self, frame) -> None:
         """of:54-62: previous gray := gray(frame 0); the vote window is emptied."""
         if self.device_ptrs:
-            N.check(self._lib.dvc_of_prime(self._h, _addr(frame), 3 * self.W))
+            N.check(self._lib.dvc_of_prime(self._h, self._dev(frame, "frame", self._fshape)[0], 3 * self.W))
         else:
-            f = self._host_frames(frame, False)
+            f = B.host_in(frame, self._fshape, "frame")
             N.check(self._lib.dvc_of_prime(self._h, f.ctypes.data, 3 * self.W))
 
     def step(self, frame, mask=None, compressed=None, want=("mask", "compressed")):
@@ -74,15 +74,14 @@ class OFWorker:
         compressed)`` (H x W {0,255} and H x W x 3); device mode writes into the
         given buffers and returns None."""
         if self.device_ptrs:
-            N.check(self._lib.dvc_of_step(self._h, _addr(frame), 3 * self.W,
-                                          _addr(mask) if mask is not None else None,
-                                          _addr(compressed) if compressed is not None else None))
+            addr = self._dev(frame, "frame", self._fshape)[0]
+            mk = self._dev(mask, "mask", (self.H, self.W))[0] if mask is not None else None
+            cp = self._dev(compressed, "compressed", self._fshape)[0] if compressed is not None else None
+            N.check(self._lib.dvc_of_step(self._h, addr, 3 * self.W, mk, cp))
             return None
-        f = self._host_frames(frame, False)
-        if mask is None and "mask" in want:
-            mask = np.empty((self.H, self.W), np.uint8)
-        if compressed is None and "compressed" in want:
-            compressed = np.empty_like(f)
+        f = B.host_in(frame, self._fshape, "frame")
+        mask = B.host_out(mask, (self.H, self.W), "mask", "mask" in want)
+        compressed = B.host_out(compressed, self._fshape, "compressed", "compressed" in want)
         N.check(self._lib.dvc_of_step(self._h, f.ctypes.data, 3 * self.W,
                                       mask.ctypes.data if mask is not None else None,
                                       compressed.ctypes.data if compressed is not None else None))
@@ -90,24 +89,23 @@ class OFWorker:
 
     def step_batch(self, frames, mask=None, compressed=None, want=("mask", "compressed")):
         """n consecutive frames (identical to n :meth:`step` calls). Host mode:
-        (n, H, W, 3) uint8 in, ``(masks, compressed)`` out. Device mode: device
-        tensors or ``(address, n)`` tuples; asynchronous, returns None."""
+        (n, H, W, 3) uint8 in, ``(masks, compressed)`` out. Device mode: CUDA
+        tensors on the handle's device or explicit ``(address, n)`` tuples;
+        asynchronous, returns None."""
         fs, ms = 3 * self.W * self.H, self.W * self.H
         if self.device_ptrs:
-            if isinstance(frames, tuple):
-                addr, n = int(frames[0]), int(frames[1])
-            else:
-                n, addr = int(frames.shape[0]), _addr(frames)
-            mk = _addr(mask[0] if isinstance(mask, tuple) else mask) if mask is not None else None
-            cp = _addr(compressed[0] if isinstance(compressed, tuple) else compressed) if compressed is not None else None
+            addr, n = self._dev(frames, "frames", self._fshape, batched=True)
+            mk = self._dev(mask, "mask", (self.H, self.W), n=n, batched=True)[0] if mask is not None else None
+            cp = self._dev(compressed, "compressed", self._fshape, n=n, batched=True)[0] \
+                if compressed is not None else None
             N.check(self._lib.dvc_of_step_batch(self._h, addr, 3 * self.W, fs, n, mk, ms, cp, fs))
             return None
-        f = self._host_frames(frames, True)
-        n = int(f.shape[0])
-        if mask is None and "mask" in want:
-            mask = np.empty((n, self.H, self.W), np.uint8)
-        if compressed is None and "compressed" in want:
-            compressed = np.empty_like(f)
+        if not isinstance(frames, np.ndarray) or frames.ndim != 4:
+            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
+        n = int(frames.shape[0])
+        f = B.host_in(frames, (n,) + self._fshape, "frames")
+        mask = B.host_out(mask, (n, self.H, self.W), "mask", "mask" in want)
+        compressed = B.host_out(compressed, f.shape, "compressed", "compressed" in want)
         N.check(self._lib.dvc_of_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, n,
                                             mask.ctypes.data if mask is not None else None, ms,
                                             compressed.ctypes.data if compressed is not None else None, fs))

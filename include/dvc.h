@@ -52,6 +52,10 @@ extern "C" {
                                      (back) kernel; read with dvc_fd_ktime()    */
 #define DVC_FLAG_KEEP_PLANES 0x4u /* keep the filtered / dilated masks of the
                                      last frame for dvc_fd_read_plane()        */
+#define DVC_FLAG_JOIN_STREAM 0x8u /* join create's hip_stream even when it is
+                                     NULL (= the legacy default stream);
+                                     without the flag NULL means "no caller
+                                     stream"                                    */
 
 /* ---- frame-differencing (FD) path ------------------------------------------ */
 
@@ -110,13 +114,18 @@ int         dvc_abi_version(void);
 const char* dvc_last_error(void);
 int         dvc_device_count(int* count);
 
-/* Create a feed handle on `device`. `hip_stream` (a hipStream_t, may be NULL for
- * a stream owned by the handle) carries prime and the contour filter; the
- * blur/threshold front, dilate + accumulate and the overlay/compress output
- * run on three internal streams, with three batches' buffers in flight; only
- * the two recurrences (previous gray, accumulated mask) are serial.
- * Device-pointer steps return after enqueueing: dvc_fd_sync (or any read-back
- * call) waits for all streams. Replaces the per-video setup at fd:56-82. */
+/* Create a feed handle on `device`. The stages run on four internal streams
+ * (blur/threshold front, contour filter, dilate + accumulate, overlay/compress
+ * output) with three batches' buffers in flight; only the two recurrences
+ * (previous gray, accumulated mask) are serial. `hip_stream` (a hipStream_t or
+ * NULL) is the caller's stream: when given, every prime/step call first waits
+ * for the work queued on it before the call (e.g. the copy producing the
+ * frames, reads of earlier outputs), and work queued on it after the call sees
+ * the call's outputs — stream-ordered use without host syncs (calls on one
+ * handle then do not overlap each other; with NULL they pipeline across calls
+ * and dvc_fd_sync is the only ordering point). Device-pointer steps return
+ * after enqueueing: dvc_fd_sync (or any read-back call) waits for all streams.
+ * Replaces the per-video setup at fd:56-82. */
 int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
 
 /* Frame 0: gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77) -> previous
@@ -228,9 +237,9 @@ typedef struct dvc_of_stats {
 /* Create an OF feed handle on `device` (GPU constraints: width and height
  * multiples of 8, morph_kernel 2, poly_n 5 or 7, winsize <= 17, window <= 127,
  * pyramid smoothing kernels <= 63 taps). Replaces the per-video setup at
- * of:38-62. `hip_stream` (NULL: a stream owned by the handle) carries prime and
- * the gray/pyramid stage; the flow and the vote/morphology/output stages run on
- * two internal streams with two batches' rings in flight. Device-pointer steps
+ * of:38-62. The gray/pyramid, flow and vote/morphology/output stages run on
+ * three internal streams with two batches' rings in flight; `hip_stream`
+ * (hipStream_t or NULL) is joined as in dvc_fd_create. Device-pointer steps
  * return after enqueueing: dvc_of_sync (or any read-back call) waits for all. */
 int dvc_of_create(const dvc_of_params* params, int device, void* hip_stream, dvc_of** out);
 

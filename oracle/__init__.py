@@ -106,6 +106,7 @@ def lib():
         L.oc_fd_step.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, u8p, u8p, u8p]
         L.oc_fd_read_plane.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p]
         L.oc_fd_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(FdStats)]
+        L.oc_fd_set_state.argtypes = [ctypes.c_void_p, u8p, u8p]
         _lib = L
     return _lib
 
@@ -317,6 +318,14 @@ class OracleFD:
         lib().oc_fd_get_stats(self._h, ctypes.byref(s))
         return {k: int(getattr(s, k)) for k, _ in FdStats._fields_}
 
+    def set_state(self, prev_gray: np.ndarray, acc: np.ndarray) -> None:
+        """Load (previous blurred gray, accumulated mask) taken from another run
+        mid-sequence: the next ``step`` checks one transition of a long run."""
+        g = np.ascontiguousarray(prev_gray, np.uint8)
+        a = np.ascontiguousarray(acc, np.uint8)
+        assert g.shape == a.shape == (self.H, self.W)
+        lib().oc_fd_set_state(self._h, _u8(g), _u8(a))
+
 
 # ------------------------------------------------------------- optical flow --
 class OfParams(ctypes.Structure):
@@ -363,6 +372,7 @@ def _of_lib():
         L.oc_of_prime.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t]
         L.oc_of_step.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, u8p, u8p, fp]
         L.oc_of_read_plane.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p]
+        L.oc_of_set_state.argtypes = [ctypes.c_void_p, u8p, u8p, ctypes.c_int]
         L.oc_farneback.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, fp]
         L.oc_morph_close_open.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
@@ -474,6 +484,14 @@ class OracleOF:
         if rc != 0:
             raise RuntimeError(f"oracle OF step failed: {rc}")
         return mask, cp, flow
+
+    def set_state(self, prev_gray: np.ndarray, raw_masks: np.ndarray) -> None:
+        """Load (previous gray, raw |flow| masks of the last frames oldest first)
+        taken from another run mid-sequence (the deque of of:84)."""
+        g = np.ascontiguousarray(prev_gray, np.uint8)
+        m = np.ascontiguousarray(raw_masks, np.uint8).reshape(-1, self.H, self.W)
+        assert g.shape == (self.H, self.W)
+        _of_lib().oc_of_set_state(self._h, _u8(g), _u8(m), int(m.shape[0]))
 
     def plane(self, which: int) -> np.ndarray:
         """0 raw |flow| mask, 1 voted, 2 close/open, 3 rectangles."""

@@ -522,3 +522,15 @@ int oc_fd_read_plane(oc_fd* h, int plane, uint8_t* dst)
 }
 
 void oc_fd_get_stats(oc_fd* h, dvc_fd_stats* out) { *out = h->st; }
+
+/* Test hook: load a feed state (the previous blurred gray, fd:133, and the
+ * accumulated mask, fd:107) taken from another implementation mid-sequence, so
+ * the next oc_fd_step checks one transition of a long run without replaying
+ * every earlier frame. */
+void oc_fd_set_state(oc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
+{
+    size_t N = (size_t)h->p.width * h->p.height;
+    memcpy(h->prev, prev_gray, N);
+    memcpy(h->acc, acc, N);
+    h->primed = 1;
+}

@@ -33,6 +33,7 @@ int oc_fd_prime(oc_fd* h, const uint8_t* bgr, size_t pitch);
 int oc_fd_step(oc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay, uint8_t* compressed, uint8_t* acc_out);
 int oc_fd_read_plane(oc_fd* h, int plane, uint8_t* dst);
 void oc_fd_get_stats(oc_fd* h, dvc_fd_stats* out);
+void oc_fd_set_state(oc_fd* h, const uint8_t* prev_gray, const uint8_t* acc);
 
 /* optical-flow path (of_oracle.c) */
 void oc_blur_f32(const float* src, int W, int H, const float* k, int n, float* dst);
@@ -56,4 +57,5 @@ void oc_of_destroy(oc_of* h);
 int oc_of_prime(oc_of* h, const uint8_t* bgr, size_t pitch);
 int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_t* compressed, float* flow);
 int oc_of_read_plane(oc_of* h, int which, uint8_t* dst);
+void oc_of_set_state(oc_of* h, const uint8_t* prev_gray, const uint8_t* raw_masks, int n);
 #endif

@@ -561,6 +561,29 @@ int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_
     return 0;
 }
 
+/* Test hook: load a feed state taken mid-sequence — the previous gray (of:101)
+ * and the raw |flow| masks of the last n frames, oldest first (the deque,
+ * of:84; nonzero = motion) — so the next oc_of_step checks one transition of a
+ * long run without replaying it. */
+void oc_of_set_state(oc_of* h, const uint8_t* prev_gray, const uint8_t* raw_masks, int n)
+{
+    size_t N = (size_t)h->p.width * h->p.height;
+    int W = h->p.window;
+    if (n > W) { raw_masks += (size_t)(n - W) * N; n = W; }
+    memcpy(h->prev, prev_gray, N);
+    for (int i = 0; i < W; ++i) memset(h->ring[i], 0, N);
+    memset(h->cnt, 0, N);
+    for (int k = 0; k < n; ++k)
+        for (size_t i = 0; i < N; ++i) {
+            uint8_t v = raw_masks[(size_t)k * N + i] ? 1 : 0;
+            h->ring[k][i] = v;
+            h->cnt[i] = (uint8_t)(h->cnt[i] + v);
+        }
+    h->L = n;
+    h->head = n % W;
+    h->primed = 1;
+}
+
 int oc_of_read_plane(oc_of* h, int which, uint8_t* dst)
 {
     size_t N = (size_t)h->p.width * h->p.height;
