@@ -21,6 +21,7 @@ HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 DVC_OK = 0
+DVC_E_ODD_DCT = -6
 DVC_FLAG_DEVICE_PTRS = 0x1
 DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
@@ -36,9 +37,9 @@ EXPORTS = [
     "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter", "dvc_fd_step_batch",
     "dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync", "dvc_of_get_stats",
     "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
-    "dvc_of_debug_read",
+    "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free",
 ]
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_BATCH = 512
 
 
@@ -67,6 +68,8 @@ class FdParams(ctypes.Structure):
         ("prime_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
         ("max_batch", ctypes.c_uint32),
+        ("src_width", ctypes.c_int32),
+        ("src_height", ctypes.c_int32),
     ]
 
 
@@ -178,6 +181,10 @@ def lib() -> ctypes.CDLL:
     L.dvc_of_destroy.restype = None
     L.dvc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                   u8p]
+    L.dvc_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
+    L.dvc_host_alloc.restype = ctypes.c_int
+    L.dvc_host_free.argtypes = [vp]
+    L.dvc_host_free.restype = None
     for name in ("dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync",
                  "dvc_of_get_stats", "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_compress"):
         getattr(L, name).restype = ctypes.c_int
@@ -195,6 +202,33 @@ def check(rc: int) -> None:
     if rc != DVC_OK:
         msg = lib().dvc_last_error()
         raise DvcError(rc, msg.decode() if msg else "")
+
+
+class _Pinned:
+    """Owner of one dvc_host_alloc block (freed when the last view dies)."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib().dvc_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def __del__(self):
+        try:
+            lib().dvc_host_free(ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
+def pinned(shape, dtype="uint8"):
+    """A numpy array in page-locked host memory (dvc_host_alloc): host-pointer
+    steps DMA such buffers directly, with no staging copy on the CPU."""
+    import numpy as np
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    owner = _Pinned(max(count * dt.itemsize, 1))
+    buf = (ctypes.c_uint8 * max(count * dt.itemsize, 1)).from_address(owner.ptr)
+    buf._owner = owner          # every view of the array keeps the block alive
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
 
 
 def contour_filter(mask, min_area2: int, device: int = 0):

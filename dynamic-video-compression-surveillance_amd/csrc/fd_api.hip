@@ -107,16 +107,34 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 }  // namespace
 
 // Buffers of one batch in flight (max_batch frames): motion masks, contour-
-// filter scratch, kept masks and the dilate -> accumulate -> out bit fields.
+// filter scratch, kept masks, the dilate -> accumulate -> out bits, and the
+// staged input frames when the caller's cannot be read in place.
 struct Slot {
     dvc::CclBufs c{};
-    uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;   // k_dilate -> k_acc -> k_out bits
+    uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;    // fast back end (B = 4, 8)
+    uint64_t *dbits = nullptr, *rbits = nullptr, *zbits = nullptr;  // generic back end (row-major planes)
+    uint8_t* fin = nullptr;    // resized / re-pitched input frames (pitch ip), allocated when needed
     hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_acc = nullptr, ev_out = nullptr;
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
 };
 
 // Batches in flight: three slots.
 constexpr int NSLOT = 3;
+
+// Host-pointer path: two staging sets, so chunk c+1's frames go up while chunk
+// c computes and chunk c-1's outputs come down.
+struct Stage {
+    uint8_t *d_in = nullptr, *d_ov = nullptr, *d_cp = nullptr;   // device
+    uint8_t *h_in = nullptr, *h_ov = nullptr, *h_cp = nullptr;   // pinned host
+    hipEvent_t ev_h2d = nullptr;   // h_in may be refilled
+    hipEvent_t ev_d2h = nullptr;   // h_ov / h_cp hold the chunk's outputs
+    hipEvent_t ev_free = nullptr;  // d_in / d_ov / d_cp may be reused
+    bool busy = false;             // ev_free / ev_d2h hold a chunk
+    int m = 0;                     // its frames
+    uint8_t *ov = nullptr, *cp = nullptr;   // its destination (pageable outputs)
+    size_t ostride = 0;
+};
+constexpr int NSTAGE = 2;
 
 struct dvc_fd {
     dvc_fd_params p{};
@@ -125,30 +143,43 @@ struct dvc_fd {
     hipStream_t user = nullptr;    // the caller's stream (create's hip_stream; NULL = legacy default)
     bool has_user = false;         // join `user` (hip_stream given, or DVC_FLAG_JOIN_STREAM)
     hipEvent_t ev_user = nullptr, ev_join_out = nullptr, ev_join_acc = nullptr;
-    hipStream_t s_front = nullptr;       // blur/threshold front (previous-gray recurrence)
+    hipStream_t s_front = nullptr;       // input staging + blur/threshold front (previous-gray recurrence)
     hipStream_t s_acc = nullptr;         // dilate + accumulate (accumulated-mask recurrence)
     hipStream_t s_out = nullptr;         // overlay + compressed frames
     dvc::RowGeom g{};
+    int gs = 0;          // gray row stride: roundup(W, 4)
+    int ip = 0;          // pitch of staged frames: 3 * gs
+    int sw = 0, sh = 0;  // source frame size (resized to W x H when different)
+    int sip = 0;         // pitch of staged source frames (host path): 3 * roundup(sw, 4)
+    bool resize = false;
+    dvc::ResizeTab rt{};
+    int B = 4, NBX = 0, NBY = 0, AP = 0;   // block size, blocks (ceil), acc pitch
+    bool fast = true;                      // B = 4, 8: block-field back end
     dvc::GaussTaps kprime{};
     dvc::DctMat M{};
+    float* Mtab = nullptr;                 // generic DCT bases (device)
     bool primed = false;
+    bool failed = false;                   // stopped at an odd-size DCT (DVC_E_ODD_DCT)
+    uint64_t err_frame = 0;
     int max_batch = 1;
     int SW = 0;          // 64-block words per block row
     size_t sstride = 0;  // static-block bit words per frame
     uint64_t frames = 0, seq = 0;  // frames stepped, batches launched
     int last_n = 0;                // frames of the last batch
     Slot slot[NSLOT];
+    Stage stage[NSTAGE];
+    int next_stage = 0;
     // device state
-    uint8_t* gray[2] = {nullptr, nullptr};  // previous blurred gray (fd:77, 133): gray[gcur]
+    uint8_t* gray[2] = {nullptr, nullptr};  // previous blurred gray (fd:77, 133): gray[gcur], rows of gs
     int gcur = 0;
-    uint8_t* acc = nullptr;        // accumulated mask (fd:81, 107)
+    uint8_t* acc = nullptr;        // accumulated mask (fd:81, 107), AP x NBY*B
     uint64_t* dbg_dil = nullptr;
     uint32_t* tmp32 = nullptr;
     uint8_t* gtmp = nullptr;
     unsigned long long* stats = nullptr;
-    // host-pointer staging (max_batch frames)
-    uint8_t *d_in = nullptr, *d_ov = nullptr, *d_cp = nullptr;
-    uint8_t *h_in = nullptr, *h_ov = nullptr, *h_cp = nullptr, *h_acc = nullptr;
+    unsigned long long* err = nullptr;  // first feed frame index with an odd static block side (~0: none)
+    uint8_t* h_acc = nullptr;
+    std::vector<void*> extra;      // lazily allocated device buffers
     // dominant-kernel timing
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
@@ -158,18 +189,26 @@ static void free_all(dvc_fd* h)
 {
     for (Slot& s : h->slot) {
         void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE,
-                       s.dblk, s.rblk, s.sbits};
+                       s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin};
         for (void* p : dev)
             if (p) (void)hipFree(p);
         for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_acc, s.ev_out})
             if (e) (void)hipEventDestroy(e);
     }
-    void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->d_in, h->d_ov, h->d_cp};
+    for (Stage& s : h->stage) {
+        for (void* p : {(void*)s.d_in, (void*)s.d_ov, (void*)s.d_cp})
+            if (p) (void)hipFree(p);
+        for (void* p : {(void*)s.h_in, (void*)s.h_ov, (void*)s.h_cp})
+            if (p) (void)hipHostFree(p);
+        for (hipEvent_t e : {s.ev_h2d, s.ev_d2h, s.ev_free})
+            if (e) (void)hipEventDestroy(e);
+    }
+    void* dev[] = {h->gray[0], h->gray[1], h->acc, h->dbg_dil, h->tmp32, h->gtmp, h->stats, h->err, h->Mtab,
+                   (void*)h->rt.xo, (void*)h->rt.yo};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* pin[] = {h->h_in, h->h_ov, h->h_cp, h->h_acc};
-    for (void* p : pin)
-        if (p) (void)hipHostFree(p);
+    for (void* p : h->extra) (void)hipFree(p);
+    if (h->h_acc) (void)hipHostFree(h->h_acc);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : {h->ev_user, h->ev_join_out, h->ev_join_acc})
         if (e) (void)hipEventDestroy(e);
@@ -215,6 +254,44 @@ static hipError_t sync_all(dvc_fd* h)
     return e;
 }
 
+// After a sync: did a frame stop at an odd-size DCT (fd:122, fd:140)?
+static int check_stop(dvc_fd* h)
+{
+    if (h->failed) return DVC_E_ODD_DCT;
+    unsigned long long e = ~0ull;
+    HIP_OK(hipMemcpy(&e, h->err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e == ~0ull) return DVC_OK;
+    h->failed = true;
+    h->err_frame = e;
+    return fail(DVC_E_ODD_DCT, "frame %llu: a static block with an odd side > 1 (OpenCV: Odd-size DCT's are not "
+                               "implemented, fd:122)", e + 1);
+}
+
+// Can the kernels read these frames in place? (dword rows reaching 3 * gs bytes)
+static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
+{
+    return !h->resize && pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 &&
+           (n <= 1 || fstride % 4 == 0);
+}
+
+static bool host_pinned(const void* p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+static hipError_t alloc_fin(dvc_fd* h)
+{
+    hipError_t e = hipSuccess;
+    for (Slot& s : h->slot)
+        if (!s.fin && e == hipSuccess) e = dalloc(&s.fin, (size_t)h->ip * h->g.H * h->max_batch);
+    return e;
+}
+
 extern "C" {
 
 int dvc_abi_version(void) { return DVC_ABI_VERSION; }
@@ -234,16 +311,30 @@ int dvc_gaussian_taps_q8(int n, double sigma, uint16_t* taps)
     return DVC_OK;
 }
 
+int dvc_host_alloc(size_t bytes, void** out)
+{
+    if (!out) return fail(DVC_E_INVALID, "NULL argument");
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(DVC_E_NOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return DVC_OK;
+}
+
+void dvc_host_free(void* p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
 int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd** out)
 {
     if (!prm || !out) return fail(DVC_E_INVALID, "NULL argument");
     const dvc_fd_params& p = *prm;
     if (p.width < 16 || p.height < 16 || p.width > 65520)
         return fail(DVC_E_INVALID, "frame %dx%d outside 16..65520 x >=16", p.width, p.height);
-    if (p.block != 4 && p.block != 8)
-        return fail(DVC_E_UNSUPPORTED, "block_size %d: the GPU path implements 4 and 8", p.block);
-    if (p.width % p.block || p.height % p.block)
-        return fail(DVC_E_UNSUPPORTED, "frame %dx%d is not a multiple of block_size %d", p.width, p.height, p.block);
+    if (p.src_width < 0 || p.src_height < 0 || p.src_width > 65520)
+        return fail(DVC_E_INVALID, "source frame %dx%d invalid", p.src_width, p.src_height);
+    if (p.block < 1 || p.block > 64)
+        return fail(DVC_E_UNSUPPORTED, "block_size %d: the GPU path implements 1..64", p.block);
     if (p.ksize < 1 || p.ksize > 63 || p.anchor < 0 || p.anchor >= p.ksize)
         return fail(DVC_E_INVALID, "dilation kernel %d (anchor %d) outside 1..63", p.ksize, p.anchor);
     if (p.ithresh < -1 || p.ithresh > 255) return fail(DVC_E_INVALID, "ithresh %d outside -1..255", p.ithresh);
@@ -258,14 +349,25 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->g.H = p.height;
     h->g.WW = (p.width + 63) / 64;
     h->g.CAP = p.width / 2 + 1;
-    h->SW = (p.width / p.block + 63) / 64;
-    h->sstride = (size_t)(p.height / p.block) * h->SW;
+    h->gs = (p.width + 3) & ~3;
+    h->ip = 3 * h->gs;
+    h->sw = p.src_width ? p.src_width : p.width;
+    h->sh = p.src_height ? p.src_height : p.height;
+    h->sip = 3 * ((h->sw + 3) & ~3);
+    h->resize = h->sw != p.width || h->sh != p.height;
+    h->B = p.block;
+    h->fast = dvc::fast_block(p.block);
+    h->NBX = (p.width + p.block - 1) / p.block;
+    h->NBY = (p.height + p.block - 1) / p.block;
+    h->AP = (h->NBX * p.block + 3) & ~3;
+    h->SW = (h->NBX + 63) / 64;
+    h->sstride = (size_t)h->NBY * h->SW;
     if (gauss_taps(p.prime_ksize, p.prime_sigma, h->kprime.t) != 0) {
         delete h;
         return fail(DVC_E_INVALID, "prime blur size %d must be odd, 1..63", p.prime_ksize);
     }
     h->kprime.n = p.prime_ksize;
-    dct_matrix(p.block, h->M);
+    if (h->fast) dct_matrix(p.block, h->M);
     auto bad = [&](hipError_t e, const char* what) {
         int rc = fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "%s: %s", what, hipGetErrorString(e));
         free_all(h);
@@ -291,6 +393,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     for (auto sp : {std::make_pair(&h->s_front, plo), std::make_pair(&h->s_acc, phi), std::make_pair(&h->s_out, 0)})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
+    const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame
     for (Slot& s : h->slot) {
         size_t sz[10];
         dvc::CclBufs::sizes(h->g, mb, sz);
@@ -299,33 +402,84 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
                            (void**)&s.c.area2, (void**)&s.c.kbits};
         for (int i = 0; i < 10; ++i)
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
-        // block fields: (W/B)(H/B) x B*B bits = W*H/8 bytes per frame <= 8*H*WW
-        if ((e = dalloc(&s.dblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&s.rblk, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if (h->fast) {   // block fields: u16 (B = 4) / u64 (B = 8) per block
+            const size_t fb = p.block == 4 ? 2 : 8;
+            if ((e = dalloc(&s.dblk, fb * nfield * mb)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = dalloc(&s.rblk, fb * nfield * mb)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        } else {
+            for (uint64_t** q : {&s.dbits, &s.rbits, &s.zbits})
+                if ((e = dalloc(q, 8 * H * WW * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        }
         for (hipEvent_t* ev : {&s.ev_front, &s.ev_ccl, &s.ev_acc, &s.ev_out})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
+    // staged input frames: always needed to resize or when rows are not whole quads
+    if (h->resize || p.width % 4) {
+        if ((e = alloc_fin(h)) != hipSuccess) return bad(e, "hipMalloc");
+    }
+    const size_t accb = (size_t)h->AP * h->NBY * p.block;
     struct { void** ptr; size_t bytes; } allocs[] = {
-        {(void**)&h->gray[0], N}, {(void**)&h->gray[1], N}, {(void**)&h->acc, N}, {(void**)&h->stats, 8 * 4 * 64},
+        {(void**)&h->gray[0], (size_t)h->gs * H}, {(void**)&h->gray[1], (size_t)h->gs * H}, {(void**)&h->acc, accb},
+        {(void**)&h->stats, 8 * 4 * 64}, {(void**)&h->err, 8},
     };
     for (auto& a : allocs)
         if ((e = dalloc(a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
     for (Slot& s : h->slot) s.c.stats = h->stats;
+    {   // DCT bases of length B, W % B, H % B (the generic back end / partial edge blocks)
+        const int B = p.block, bw = p.width % B, bh = p.height % B;
+        std::vector<float> tab((size_t)B * B + bw * bw + bh * bh);
+        auto basis = [](int n, float* m) {
+            const double PI = 3.14159265358979323846;
+            for (int k = 0; k < n; ++k)
+                for (int j = 0; j < n; ++j) {
+                    const double c = k == 0 ? std::sqrt(1.0 / n) : std::sqrt(2.0 / n);
+                    m[k * n + j] = (float)(c * std::cos(PI * (2 * j + 1) * k / (2.0 * n)));
+                }
+        };
+        basis(B, tab.data());
+        if (bw) basis(bw, tab.data() + B * B);
+        if (bh) basis(bh, tab.data() + B * B + bw * bw);
+        if ((e = dalloc(&h->Mtab, 4 * tab.size())) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = hipMemcpy(h->Mtab, tab.data(), 4 * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
+            return bad(e, "hipMemcpy");
+    }
+    if (h->resize) {
+        std::vector<int> tx(3 * W), ty(3 * H);
+        dvc::resize_tables(h->sw, h->sh, p.width, p.height, tx.data(), ty.data(), &h->rt.area2x, &h->rt.simd_end);
+        h->rt.sw = h->sw;
+        h->rt.sh = h->sh;
+        h->rt.dw = p.width;
+        h->rt.dh = p.height;
+        int *dx = nullptr, *dy = nullptr;
+        if ((e = dalloc(&dx, 4 * tx.size())) != hipSuccess) return bad(e, "hipMalloc");
+        h->rt.xo = dx;
+        if ((e = dalloc(&dy, 4 * ty.size())) != hipSuccess) return bad(e, "hipMalloc");
+        h->rt.yo = dy;
+        if ((e = hipMemcpy(dx, tx.data(), 4 * tx.size(), hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+        if ((e = hipMemcpy(dy, ty.data(), 4 * ty.size(), hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+    }
     if (p.flags & DVC_FLAG_KEEP_PLANES) {
         if ((e = dalloc(&h->dbg_dil, 8 * H * WW)) != hipSuccess) return bad(e, "hipMalloc");
     }
     if (!(p.flags & DVC_FLAG_DEVICE_PTRS)) {
-        const size_t F = 3 * N * (size_t)mb;
-        if ((e = dalloc(&h->d_in, F)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&h->d_ov, F)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = dalloc(&h->d_cp, F)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_in, F)) != hipSuccess) return bad(e, "hipHostMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_ov, F)) != hipSuccess) return bad(e, "hipHostMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_cp, F)) != hipSuccess) return bad(e, "hipHostMalloc");
+        const size_t Fi = (size_t)h->sip * h->sh * mb, Fo = 3 * N * (size_t)mb;
+        for (Stage& st : h->stage) {
+            if ((e = dalloc(&st.d_in, Fi)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = dalloc(&st.d_ov, Fo)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = dalloc(&st.d_cp, Fo)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = hipHostMalloc((void**)&st.h_in, Fi)) != hipSuccess) return bad(e, "hipHostMalloc");
+            if ((e = hipHostMalloc((void**)&st.h_ov, Fo)) != hipSuccess) return bad(e, "hipHostMalloc");
+            if ((e = hipHostMalloc((void**)&st.h_cp, Fo)) != hipSuccess) return bad(e, "hipHostMalloc");
+            for (hipEvent_t* ev : {&st.ev_h2d, &st.ev_d2h, &st.ev_free})
+                if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+        }
         if ((e = hipHostMalloc((void**)&h->h_acc, N)) != hipSuccess) return bad(e, "hipHostMalloc");
     }
     if ((e = hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    if ((e = hipMemsetAsync(h->err, 0xff, 8, h->stream)) != hipSuccess) return bad(e, "hipMemset");
+    // the acc padding of partial blocks stays 0 for good
+    if ((e = hipMemsetAsync(h->acc, 0, accb, h->stream)) != hipSuccess) return bad(e, "hipMemset");
     // the OUTSIDE gap node of every frame slice is its own root before any
     // k_band runs (its over-budget path may walk through it)
     for (Slot& s : h->slot) {
@@ -338,56 +492,107 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     return DVC_OK;
 }
 
+}  // extern "C"
+
+// Frames the kernels read: the caller's in place, or staged into slot S's
+// buffer on s_front (re-pitched, or resized — cv2.resize, fd:74,91). The
+// staged buffer is rewritten only after the slot's previous batch is out.
+static int stage_input(dvc_fd* h, Slot& S, const uint8_t* src, size_t pitch, size_t fstride, int n,
+                       const uint8_t** d, int* dp, size_t* dfs)
+{
+    if (direct_frames(h, src, pitch, fstride, n)) {
+        *d = src;
+        *dp = (int)pitch;
+        *dfs = fstride;
+        return DVC_OK;
+    }
+    if (!S.fin) HIP_OK(alloc_fin(h));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
+    const size_t H = h->g.H, fs = (size_t)h->ip * H;
+    if (h->resize) {
+        HIP_OK(dvc::launch_resize(src, (int)pitch, fstride, S.fin, h->ip, fs, n, h->rt, h->s_front));
+    } else if (n == 1 || fstride == pitch * H) {
+        HIP_OK(hipMemcpy2DAsync(S.fin, h->ip, src, pitch, 3 * (size_t)h->g.W, H * n, hipMemcpyDeviceToDevice,
+                                h->s_front));
+    } else {
+        for (int t = 0; t < n; ++t)
+            HIP_OK(hipMemcpy2DAsync(S.fin + t * fs, h->ip, src + t * fstride, pitch, 3 * (size_t)h->g.W, H,
+                                    hipMemcpyDeviceToDevice, h->s_front));
+    }
+    *d = S.fin;
+    *dp = h->ip;
+    *dfs = fs;
+    return DVC_OK;
+}
+
+extern "C" {
+
 int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 {
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
-    if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (pitch < 3 * (size_t)h->sw) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
-    const size_t W = h->p.width, H = h->p.height, N = W * H;
+    const size_t W = h->p.width, H = h->p.height;
     if (!h->tmp32) {
-        HIP_OK(dalloc(&h->tmp32, 4 * N));
-        HIP_OK(dalloc(&h->gtmp, N));
+        HIP_OK(dalloc(&h->tmp32, 4 * W * H));
+        HIP_OK(dalloc(&h->gtmp, (size_t)h->gs * H));
     }
     HIP_OK(sync_all(h));  // no batch of a previous run may still be in flight
     HIP_OK(wait_user(h));
-    const uint8_t* d = bgr;
-    int dp = (int)pitch;
-    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
-        for (size_t y = 0; y < H; ++y) std::memcpy(h->h_in + y * 3 * W, bgr + y * pitch, 3 * W);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, 3 * N, hipMemcpyHostToDevice, h->stream));
-        d = h->d_in;
-        dp = (int)(3 * W);
-    }
-    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->gcur], h->p.width, h->p.height, h->kprime, h->stream));
-    HIP_OK(hipMemsetAsync(h->acc, 0, N, h->stream));
-    HIP_OK(hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->stream));
-    HIP_OK(hipStreamSynchronize(h->stream));
     for (Slot& s : h->slot) s.recorded = false;
+    for (Stage& s : h->stage) s.busy = false;
+    const uint8_t* src = bgr;
+    size_t sp = pitch;
+    if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
+        Stage& st = h->stage[0];
+        for (int y = 0; y < h->sh; ++y) std::memcpy(st.h_in + (size_t)y * h->sip, bgr + y * pitch, 3 * (size_t)h->sw);
+        HIP_OK(hipMemcpyAsync(st.d_in, st.h_in, (size_t)h->sip * h->sh, hipMemcpyHostToDevice, h->s_front));
+        src = st.d_in;
+        sp = h->sip;
+    }
+    const uint8_t* d = nullptr;
+    int dp = 0;
+    size_t dfs = 0;
+    int rc = stage_input(h, h->slot[0], src, sp, 0, 1, &d, &dp, &dfs);
+    if (rc) return rc;
+    HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->gcur], h->p.width, h->p.height, h->gs, h->kprime,
+                             h->s_front));
+    HIP_OK(hipMemsetAsync(h->acc, 0, (size_t)h->AP * h->NBY * h->B, h->s_front));
+    HIP_OK(hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->s_front));
+    HIP_OK(hipMemsetAsync(h->err, 0xff, 8, h->s_front));
+    HIP_OK(hipStreamSynchronize(h->s_front));
     h->frames = 0;
     h->seq = 0;
     h->last_n = 0;
     h->primed = true;
+    h->failed = false;
+    h->err_frame = 0;
     return DVC_OK;
 }
 
 }  // extern "C"
 
-// Enqueue one batch i of n <= max_batch device-resident frames, slot S = i % 3
-// (j = i - 3 = the slot's previous batch):
-//   s_front:         [wait ccl(j)]            front(i) -> ev_front   (S.mbits free)
+// Enqueue one batch i of n <= max_batch frames, slot S = i % 3 (j = i - 3 =
+// the slot's previous batch):
+//   s_front:         [wait ccl(j) (+ out(j) when staging)]  stage, front(i) -> ev_front   (S.mbits free)
 //   stream:          [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
 //   s_acc:           [wait ev_ccl, out(j)]    dilate + accumulate(i) -> ev_acc (S bits free)
 //   s_out:           [wait ev_acc]            k_out(i) -> ev_out
 // so front(i+2), the contour filter of i+1, the accumulation of i and the
 // output of i-1 can all be in flight; the two recurrences (previous gray,
 // accumulated mask) are serial, each on its own stream.
-static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
+static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride)
 {
     Slot& S = h->slot[h->seq % NSLOT];
     hipStream_t s_ccl = h->stream;
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
-    HIP_OK(dvc::launch_front(d, dp, fstride, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], S.c.mbits, h->g,
+    const uint8_t* d = nullptr;
+    int dp = 0;
+    size_t dfs = 0;
+    int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs);
+    if (rc) return rc;
+    HIP_OK(dvc::launch_front(d, dp, dfs, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
                              h->p.ithresh, h->s_front));
     HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
@@ -401,18 +606,26 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     a.g = h->g;
     a.bgr = d;
     a.pitch = dp;
-    a.fstride = fstride;
+    a.fstride = dfs;
     a.acc = h->acc;
+    a.ap = h->AP;
     a.overlay = ov;
     a.compressed = cp;
     a.opitch = 3 * h->p.width;
     a.ostride = ostride;
+    a.obytes = (a.opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
     a.kbits = S.c.kbits;
     a.dblk = S.dblk;
     a.rblk = S.rblk;
     a.sbits = S.sbits;
     a.SW = h->SW;
     a.sstride = h->sstride;
+    a.dbits = S.dbits;
+    a.rbits = S.rbits;
+    a.zbits = S.zbits;
+    a.B = h->B;
+    a.NBX = h->NBX;
+    a.NBY = h->NBY;
     a.n = n;
     a.ksize = h->p.ksize;
     a.anchor = h->p.anchor;
@@ -426,8 +639,11 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
         a.acc0_fixed = z < 0.5f && z > -0.5f;  // saturate_cast<uchar>(0) == 0 (NaN/negatives excluded)
     }
     a.M = h->M;
+    a.Mtab = h->Mtab;
     a.stats = h->stats;
     a.dbg_dil = h->dbg_dil;
+    a.err = h->err;
+    a.frame0 = h->frames;
     // KTIMING: events around k_out (the HBM-bound kernel) on s_out
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
     if (timed) {
@@ -437,11 +653,11 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::launch_accumulate(a, h->p.block, h->s_acc));
+    HIP_OK(dvc::launch_accumulate(a, h->s_acc));
     HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
     HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
-    HIP_OK(dvc::launch_out(a, h->p.block, h->s_out));
+    HIP_OK(dvc::launch_out(a, h->s_out));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
         h->ev_used += 2;
@@ -454,58 +670,108 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* d, int dp, size_t fstride, in
     return DVC_OK;
 }
 
-// n frames in chunks of max_batch; host pointers are staged through the pinned
-// buffers (each chunk completes before the call returns).
+// Host-pointer chunk finished on the device: copy its pageable outputs out.
+static int drain_stage(dvc_fd* h, Stage& st)
+{
+    if (!st.busy) return DVC_OK;
+    HIP_OK(hipEventSynchronize(st.ev_d2h));
+    const size_t N3 = 3 * (size_t)h->p.width * h->p.height;
+    for (int t = 0; t < st.m; ++t) {
+        if (st.ov) std::memcpy(st.ov + (size_t)t * st.ostride, st.h_ov + (size_t)t * N3, N3);
+        if (st.cp) std::memcpy(st.cp + (size_t)t * st.ostride, st.h_cp + (size_t)t * N3, N3);
+    }
+    st.busy = false;
+    return DVC_OK;
+}
+
+// n frames in chunks of max_batch. Device pointers: enqueued, asynchronous.
+// Host pointers: two staging sets pipeline the chunks — the frames of chunk
+// c+1 are copied into pinned memory and sent up while chunk c computes and
+// chunk c-1's outputs come down; pinned caller buffers (dvc_host_alloc) are
+// DMA'd directly with no CPU copy. Returns once every output has landed.
 static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstride, int n, uint8_t* overlay,
                       uint8_t* compressed, size_t ostride, uint8_t* acc_out)
 {
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
     if (!h->primed) return fail(DVC_E_STATE, "step before dvc_fd_prime");
+    if (h->failed) return fail(DVC_E_STATE, "the feed stopped at an odd-size DCT (frame %llu); prime again",
+                               (unsigned long long)h->err_frame + 1);
     if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
-    const size_t W = h->p.width, H = h->p.height, N = W * H, row = 3 * W;
-    if (pitch < row || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    if (n > 1 && (fstride < pitch * (H - 1) + row || fstride % 4))
-        return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
-    if (n > 1 && (overlay || compressed) && (ostride < 3 * N || ostride % 4))
+    const size_t W = h->p.width, H = h->p.height, N = W * H, srow = 3 * (size_t)h->sw;
+    if (pitch < srow) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (n > 1 && fstride < pitch * (h->sh - 1) + srow) return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
+    if (n > 1 && (overlay || compressed) && ostride < 3 * N)
         return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(wait_user(h));
     const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
+    if (devp) {
+        for (int f0 = 0; f0 < n; f0 += h->max_batch) {
+            const int m = std::min(h->max_batch, n - f0);
+            int rc = enqueue_batch(h, bgr + (size_t)f0 * fstride, pitch, fstride, m,
+                                   overlay ? overlay + (size_t)f0 * ostride : nullptr,
+                                   compressed ? compressed + (size_t)f0 * ostride : nullptr, ostride);
+            if (rc) return rc;
+        }
+        if (acc_out) HIP_OK(hipMemcpy2DAsync(acc_out, W, h->acc, h->AP, W, H, hipMemcpyDeviceToDevice, h->s_acc));
+        HIP_OK(join_user(h));
+        return DVC_OK;
+    }
+    const bool pin_in = host_pinned(bgr);
+    const bool pin_out = (!overlay || host_pinned(overlay)) && (!compressed || host_pinned(compressed));
+    const size_t N3 = 3 * N, sfs = (size_t)h->sip * h->sh;
     for (int f0 = 0; f0 < n; f0 += h->max_batch) {
         const int m = std::min(h->max_batch, n - f0);
+        Stage& st = h->stage[h->next_stage];
+        h->next_stage = (h->next_stage + 1) % NSTAGE;
+        int rc = drain_stage(h, st);   // the chunk that used this set two chunks ago
+        if (rc) return rc;
         const uint8_t* in = bgr + (size_t)f0 * fstride;
         uint8_t* ov = overlay ? overlay + (size_t)f0 * ostride : nullptr;
         uint8_t* cp = compressed ? compressed + (size_t)f0 * ostride : nullptr;
-        if (devp) {
-            int rc = enqueue_batch(h, in, (int)pitch, fstride, m, ov, cp, ostride);
-            if (rc) return rc;
-            continue;
+        HIP_OK(hipStreamWaitEvent(h->s_front, st.ev_free, 0));   // d_in / d_ov / d_cp of two chunks ago are done
+        if (pin_in) {
+            for (int t = 0; t < m; ++t)
+                HIP_OK(hipMemcpy2DAsync(st.d_in + t * sfs, h->sip, in + (size_t)t * fstride, pitch, srow, h->sh,
+                                        hipMemcpyHostToDevice, h->s_front));
+        } else {
+            HIP_OK(hipEventSynchronize(st.ev_h2d));   // h_in's previous upload is done
+            for (int t = 0; t < m; ++t)
+                for (int y = 0; y < h->sh; ++y)
+                    std::memcpy(st.h_in + t * sfs + (size_t)y * h->sip, in + (size_t)t * fstride + (size_t)y * pitch,
+                                srow);
+            HIP_OK(hipMemcpyAsync(st.d_in, st.h_in, (size_t)m * sfs, hipMemcpyHostToDevice, h->s_front));
+            HIP_OK(hipEventRecord(st.ev_h2d, h->s_front));
         }
-        for (int t = 0; t < m; ++t)
-            for (size_t y = 0; y < H; ++y)
-                std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_front));
-        int rc = enqueue_batch(h, h->d_in, (int)row, 3 * N, m, ov ? h->d_ov : nullptr, cp ? h->d_cp : nullptr, 3 * N);
+        rc = enqueue_batch(h, st.d_in, h->sip, sfs, m, ov ? st.d_ov : nullptr, cp ? st.d_cp : nullptr, N3);
         if (rc) return rc;
-        if (ov) HIP_OK(hipMemcpyAsync(h->h_ov, h->d_ov, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_out));
-        if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_out));
-        HIP_OK(sync_all(h));
-        for (int t = 0; t < m; ++t) {
-            if (ov) std::memcpy(ov + (size_t)t * ostride, h->h_ov + (size_t)t * 3 * N, 3 * N);
-            if (cp) std::memcpy(cp + (size_t)t * ostride, h->h_cp + (size_t)t * 3 * N, 3 * N);
+        if (pin_out) {
+            if (ov) HIP_OK(hipMemcpy2DAsync(ov, ostride, st.d_ov, N3, N3, m, hipMemcpyDeviceToHost, h->s_out));
+            if (cp) HIP_OK(hipMemcpy2DAsync(cp, ostride, st.d_cp, N3, N3, m, hipMemcpyDeviceToHost, h->s_out));
+        } else {
+            if (ov) HIP_OK(hipMemcpyAsync(st.h_ov, st.d_ov, (size_t)m * N3, hipMemcpyDeviceToHost, h->s_out));
+            if (cp) HIP_OK(hipMemcpyAsync(st.h_cp, st.d_cp, (size_t)m * N3, hipMemcpyDeviceToHost, h->s_out));
         }
+        HIP_OK(hipEventRecord(st.ev_d2h, h->s_out));
+        HIP_OK(hipEventRecord(st.ev_free, h->s_out));
+        st.busy = !pin_out && (ov || cp);
+        st.m = m;
+        st.ov = ov;
+        st.cp = cp;
+        st.ostride = ostride;
+    }
+    for (Stage& st : h->stage) {
+        int rc = drain_stage(h, st);
+        if (rc) return rc;
     }
     if (acc_out) {
-        if (devp) {
-            HIP_OK(hipMemcpyAsync(acc_out, h->acc, N, hipMemcpyDeviceToDevice, h->s_acc));
-        } else {
-            HIP_OK(hipMemcpyAsync(h->h_acc, h->acc, N, hipMemcpyDeviceToHost, h->s_acc));
-            HIP_OK(hipStreamSynchronize(h->s_acc));
-            std::memcpy(acc_out, h->h_acc, N);
-        }
+        HIP_OK(hipMemcpy2DAsync(h->h_acc, W, h->acc, h->AP, W, H, hipMemcpyDeviceToHost, h->s_acc));
+        HIP_OK(hipStreamSynchronize(h->s_acc));
+        std::memcpy(acc_out, h->h_acc, N);
     }
+    HIP_OK(sync_all(h));
     HIP_OK(join_user(h));
-    return DVC_OK;
+    return check_stop(h);
 }
 
 extern "C" {
@@ -527,7 +793,7 @@ int dvc_fd_sync(dvc_fd* h)
     if (!h) return fail(DVC_E_INVALID, "NULL handle");
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(sync_all(h));
-    return DVC_OK;
+    return check_stop(h);
 }
 
 int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out)
@@ -535,10 +801,11 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out)
     if (!h || !out) return fail(DVC_E_INVALID, "NULL argument");
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(sync_all(h));
+    (void)check_stop(h);
     unsigned long long slots[64 * 4], s[4] = {0, 0, 0, 0};
     HIP_OK(hipMemcpy(slots, h->stats, sizeof(slots), hipMemcpyDeviceToHost));
     for (int i = 0; i < 64 * 4; ++i) s[i % 4] += slots[i];
-    out->frames = h->frames;
+    out->frames = h->failed ? std::min<uint64_t>(h->frames, h->err_frame) : h->frames;
     out->motion_px = s[1];
     out->components = s[2];
     out->static_blocks = s[3];
@@ -548,12 +815,18 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out)
 int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* dst)
 {
     if (!h || !dst) return fail(DVC_E_INVALID, "NULL argument");
-    if (!h->frames) return fail(DVC_E_STATE, "no frame stepped yet");
+    if (!h->primed) return fail(DVC_E_STATE, "read_plane before dvc_fd_prime");
+    if (!h->frames && plane != DVC_PLANE_GRAY && plane != DVC_PLANE_ACC)
+        return fail(DVC_E_STATE, "no frame stepped yet");
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(sync_all(h));
-    const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
-    if (plane == DVC_PLANE_GRAY || plane == DVC_PLANE_ACC) {
-        HIP_OK(hipMemcpy(dst, plane == DVC_PLANE_GRAY ? h->gray[h->gcur] : h->acc, N, hipMemcpyDeviceToHost));
+    const size_t W = h->p.width, H = h->p.height, WW = h->g.WW;
+    if (plane == DVC_PLANE_GRAY) {
+        HIP_OK(hipMemcpy2D(dst, W, h->gray[h->gcur], h->gs, W, H, hipMemcpyDeviceToHost));
+        return DVC_OK;
+    }
+    if (plane == DVC_PLANE_ACC) {
+        HIP_OK(hipMemcpy2D(dst, W, h->acc, h->AP, W, H, hipMemcpyDeviceToHost));
         return DVC_OK;
     }
     // the last frame of the last batch
@@ -601,8 +874,8 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
                        uint8_t* filtered, uint64_t* components)
 {
     if (!mask || !filtered) return fail(DVC_E_INVALID, "NULL argument");
-    if (width < 4 || height < 4 || width % 4 || height % 4 || width > 65520)
-        return fail(DVC_E_INVALID, "mask %dx%d: sides must be multiples of 4", width, height);
+    if (width < 4 || height < 4 || width > 65520)
+        return fail(DVC_E_INVALID, "mask %dx%d: sides must be 4..65520", width, height);
     HIP_OK(hipSetDevice(device));
     dvc::RowGeom g{width, height, (width + 63) / 64, width / 2 + 1};
     const size_t W = width, H = height, N = W * H, WW = g.WW, CAP = g.CAP;

@@ -61,43 +61,80 @@ struct CclBufs {
     }
 };
 
+// The back of the loop (dilate, accumulate, overlay, compress). Blocks are
+// B x B (fd:117-118); NBX x NBY of them cover the frame, the last column / row
+// partial when W % B or H % B (fd:120-121). Two layouts:
+//  * fast (B = 4, 8): block-major bit fields per frame (k_dilate -> k_acc ->
+//    k_out, one lane per block), acc padded to NBX*B x NBY*B;
+//  * generic (any other B, and the partial edge blocks of the fast layout):
+//    row-major H x WW bit planes (k_dilate_rows -> k_acc_rows -> k_out_gen,
+//    LDS-staged block DCTs of any shape).
 struct BackArgs {
     RowGeom g;
-    const uint8_t* bgr;   // frame t at bgr + t * fstride, rows of `pitch` bytes
+    const uint8_t* bgr;   // frame t at bgr + t * fstride, rows of `pitch` bytes (pitch % 4 == 0)
     int pitch;
     size_t fstride;
-    uint8_t* acc;         // read before frame 0, written after frame n-1
+    uint8_t* acc;         // read before frame 0, written after frame n-1; rows of `ap` bytes
+    int ap;
     uint8_t* overlay;     // nullable; frame t at overlay + t * ostride, rows of opitch
     uint8_t* compressed;  // nullable; same layout
     int opitch;
     size_t ostride;
+    int obytes;             // outputs not 4-byte aligned: byte stores
     const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
+    // fast layout
     void* dblk;             // dilated mask, block-major BxB bit fields per frame (k_dilate -> k_acc)
     void* rblk;             // acc > 127 per pixel, block-major BxB bit fields per frame (k_acc -> k_out)
-    uint64_t* sbits;        // acc all zero per block, (H/B) x SW per frame (k_acc -> k_out)
-    int SW;                 // 64-block words per block row = ceil(W/B/64)
-    size_t sstride;         // (H/B) * SW
+    uint64_t* sbits;        // acc all zero per block, NBY x SW per frame (k_acc -> k_out)
+    int SW;                 // 64-block words per block row = ceil(NBX/64)
+    size_t sstride;         // NBY * SW
+    // generic layout (row-major H x WW words per frame)
+    uint64_t* dbits;        // dilated mask
+    uint64_t* rbits;        // acc > 127
+    uint64_t* zbits;        // acc != 0
+    int B, NBX, NBY;        // block size, blocks across / down (ceil)
     int n;                  // frames in the batch
     int ksize, anchor;
     float alpha, beta, gamma, quant;
     double qinv;            // RN53(1 / (double)quant): the quantiser division as a product (div_rn)
     int acc0_fixed;         // addWeighted(acc 0, dilated 0) == 0: zero blocks stay zero
-    DctMat M;
+    DctMat M;               // fast B x B basis (kernargs)
+    const float* Mtab;      // generic bases in device memory: M_B (B*B) | M_{W%B} | M_{H%B}
     unsigned long long* stats;
-    uint64_t* dbg_dil;   // nullable: dilated mask bits of frame n-1
+    uint64_t* dbg_dil;      // nullable: dilated mask bits of frame n-1 (H x WW)
+    unsigned long long* err;  // first frame (feed index) with an odd static block side > 1 (atomicMin)
+    unsigned long long frame0;  // feed index of the batch's frame 0
 };
 
+// Gray planes (prev gray, the prime's scratch) have rows of gs = roundup(W, 4)
+// bytes; frames read by the kernels have pitch % 4 == 0 and pitch >= 3 * gs.
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
-                        int W, int H, const GaussTaps& k, hipStream_t s);
+                        int W, int H, int gs, const GaussTaps& k, hipStream_t s);
 // frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
 // gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
-                        uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
+                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
+// cv2.resize(frame, (W, H)) INTER_LINEAR 8UC3 (fd:74,91) of n frames into dst
+// (rows of dpitch, frames of dstride). Tables from resize_tables().
+struct ResizeTab {
+    int sw, sh, dw, dh;
+    int area2x;             // exact 2x downscale: OpenCV's INTER_AREA fast path
+    int simd_end;           // bytes of a row done by the 128-bit SIMD formula (VResizeLinearVec_32s8u)
+    const int* xo;          // per output column: source column, alpha0, alpha1 (device, 3*dw)
+    const int* yo;          // per output row: source row, beta0, beta1 (device, 3*dh)
+};
+void resize_tables(int sw, int sh, int dw, int dh, int* host_x /* 3*dw */, int* host_y /* 3*dh */, int* area2x,
+                   int* simd_end);
+hipError_t launch_resize(const uint8_t* src, int spitch, size_t sstride, uint8_t* dst, int dpitch, size_t dstride,
+                         int n, const ResizeTab& t, hipStream_t s);
 int band_rows(const RowGeom& g);
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
 // k_dilate then k_acc (the accumulated-mask recurrence: batches in order)
-hipError_t launch_accumulate(const BackArgs& a, int block, hipStream_t s);
-// k_out (overlay + compressed frames; no recurrence, nothing if both are NULL)
-hipError_t launch_out(const BackArgs& a, int block, hipStream_t s);
+hipError_t launch_accumulate(const BackArgs& a, hipStream_t s);
+// k_out (overlay + compressed frames; no recurrence) and k_out_gen for the
+// generic layout / partial edge blocks (always launched: it also detects the
+// odd-size DCT stop and counts generic static blocks)
+hipError_t launch_out(const BackArgs& a, hipStream_t s);
+inline bool fast_block(int B) { return B == 4 || B == 8; }
 
 }  // namespace dvc

@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "dvc_device.h"
@@ -36,36 +37,38 @@
 namespace dvc {
 
 // ------------------------------------------------------------ prime (fd:77) -
+// gray rows of gs = roundup(W, 4) bytes; the last quad of a row may be partial
+// (its bytes past W are don't-care padding, read from the padded frame row)
 __global__ void __launch_bounds__(256) k_gray(const uint8_t* __restrict__ bgr, int pitch,
-                                              uint8_t* __restrict__ gray, int W, int H)
+                                              uint8_t* __restrict__ gray, int W, int H, int gs)
 {
     int q = blockIdx.x * 256 + threadIdx.x;  // quad index in the row
     int y = blockIdx.y;
     if (4 * q >= W) return;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(bgr + (size_t)y * pitch + 12 * q);
-    *reinterpret_cast<uint32_t*>(gray + (size_t)y * W + 4 * q) = gray4(p[0], p[1], p[2]);
+    *reinterpret_cast<uint32_t*>(gray + (size_t)y * gs + 4 * q) = gray4(p[0], p[1], p[2]);
 }
 
 __global__ void __launch_bounds__(256) k_hblur_q8(const uint8_t* __restrict__ src, uint32_t* __restrict__ tmp,
-                                                  int W, int H, GaussTaps k)
+                                                  int W, int H, int gs, GaussTaps k)
 {
     int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
     int r = k.n / 2;
     uint32_t s = 0;
-    for (int j = 0; j < k.n; ++j) s += (uint32_t)k.t[j] * src[(size_t)y * W + reflect101(x + j - r, W)];
+    for (int j = 0; j < k.n; ++j) s += (uint32_t)k.t[j] * src[(size_t)y * gs + reflect101(x + j - r, W)];
     tmp[(size_t)y * W + x] = s;
 }
 
 __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ tmp, uint8_t* __restrict__ dst,
-                                                  int W, int H, GaussTaps k)
+                                                  int W, int H, int gs, GaussTaps k)
 {
     int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= W) return;
     int r = k.n / 2;
     uint64_t s = 0;
     for (int i = 0; i < k.n; ++i) s += (uint64_t)k.t[i] * tmp[(size_t)reflect101(y + i - r, H) * W + x];
-    dst[(size_t)y * W + x] = (uint8_t)((s + 32768u) >> 16);
+    dst[(size_t)y * gs + x] = (uint8_t)((s + 32768u) >> 16);
 }
 
 // ------------------------------------------------------------------ front ---
@@ -93,7 +96,7 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 // The previous blurred gray (fd:133) stays in registers as two u16 pairs.
 __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
                                                int chunk, const uint8_t* __restrict__ gray_in,
-                                               uint8_t* __restrict__ gray_out, uint64_t* __restrict__ mbits,
+                                               uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                int W, int H, int WW, int ithresh)
 {
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
@@ -109,13 +112,15 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     // Every load below is unconditional from a clamped, always-valid address
     // (the value is discarded where it is not needed): a conditional load makes
     // hipcc branch around it and drain vmcnt to 0 before the next one.
-    // previous blurred gray of this lane's 4 output rows, as u16 pairs
-    const int xc = x + 3 < W ? x : W - 4;
+    // previous blurred gray of this lane's 4 output rows, as u16 pairs. The
+    // quad holding px W-1 may be partial (W % 4): it is loaded in place (frame
+    // rows are padded to 3 * gs bytes); quads past it reload the last quad.
+    const int xc = x < W ? x : gs - 4;
     u16x2 pl[FT_H / 4], ph[FT_H / 4];
 #pragma unroll
     for (int i = 0; i < FT_H / 4; ++i) {
         const int y = min(y0 + wave + 4 * i, H - 1);
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * W + xc);
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * gs + xc);
         pl[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c010c00u));
         ph[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c02u));
     }
@@ -132,7 +137,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const int hr = lane >> 1, hs = lane & 1;
     const int hx = x0 + (hs ? FT_W : -4);
     const uint32_t hoff = (uint32_t)(reflect1(y0 - 2 + min(hr, FT_R - 1), H) * pitch +
-                                     3 * (hx >= 0 && hx + 3 < W ? hx : xc));
+                                     3 * (hx >= 0 && hx < W ? hx : xc));
     uint32_t v0[NR], v1[NR], v2[NR], h0, h1, h2;
     auto load = [&](const uint8_t* f) {
 #pragma unroll
@@ -145,12 +150,13 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     };
     load(bgr + (size_t)t_begin * fstride);
 
-    // BORDER_REFLECT_101 columns: the halo quad left of x = 0 and the quad at
-    // x = W (when it lies in this tile) are byte permutations of their
-    // neighbours, fixed up in LDS after the straight loads land.
+    // BORDER_REFLECT_101 columns: the halo quad left of x = 0 and px W, W+1
+    // (when they lie in this tile's LDS columns) are copies of px 4..1 and
+    // W-2, W-3, fixed up in LDS after the straight loads land. LDS byte b of
+    // quad column c holds px x0 - 4 + 4c + b.
     const bool fix_l = x0 == 0;
-    const int qe = (W - x0) / 4 + 1;              // LDS quad index of px W
-    const bool fix_r = qe < FT_Q;
+    const int iW = W - x0 + 4;                    // LDS byte index of px W
+    const bool fix_r = iW < 4 * FT_Q;
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
     for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
@@ -167,10 +173,11 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
                     sg[tid][0] = (b & 255) | (((a >> 24) & 255) << 8) | (((a >> 16) & 255) << 16) | (((a >> 8) & 255) << 24);
                 }
             } else if (tid >= 64 && tid < 64 + FT_R) {
-                if (fix_r) {             // px W, W+1 = px W-2, W-3 (bytes 2, 3 are never read)
-                    const int r = tid - 64;
-                    const uint32_t a = sg[r][qe - 1], b = sg[r][qe - 2];
-                    sg[r][qe] = ((a >> 16) & 255) | (((a >> 8) & 255) << 8) | ((a & 255) << 16) | ((b >> 24) << 24);
+                if (fix_r) {             // px W, W+1 = px W-2, W-3 (later bytes are never read)
+                    uint8_t* row = reinterpret_cast<uint8_t*>(&sg[tid - 64][0]);
+                    const uint8_t a = row[iW - 2], b = row[iW - 3];
+                    row[iW] = a;
+                    if (iW + 1 < 4 * FT_Q) row[iW + 1] = b;
                 }
             }
         }
@@ -216,6 +223,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
             pl[i] = gl;
             ph[i] = gh;
             if (y >= H || x >= W || t < t_first) nib = 0;
+            if (x + 4 > W) nib &= (1u << max(W - x, 0)) - 1u;   // partial quad: px >= W are not pixels
             // 8 lanes x 4 px = one 32-bit half of a mask word: OR-reduce within
             // each group of 8 lanes with DPP (quad_perm xor 1, xor 2, row_half_mirror)
             uint32_t w = nib << (4 * (lane & 7));
@@ -233,7 +241,7 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
         for (int i = 0; i < FT_H / 4; ++i) {
             const int y = y0 + wave + 4 * i;
             if (y < H && x < W)
-                *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * W + x) =
+                *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * gs + x) =
                     __builtin_amdgcn_perm(as_u32(ph[i]), as_u32(pl[i]), 0x06040200u);
         }
     }
@@ -640,13 +648,14 @@ template <int B>
 __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
 {
     typedef typename BlkT<B>::T BT;
-    const int W = a.g.W, H = a.g.H, WW = a.g.WW, NBX = W / B;
-    const int NBY = H / B;
+    const int W = a.g.W, H = a.g.H, WW = a.g.WW, NBX = a.NBX, NBY = a.NBY;
     const int idx = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y;
     if (idx >= WW * NBY) return;
     const int wi = idx % WW, by = idx / WW, y0 = by * B;
     const int k = a.ksize, an = a.anchor;
     const uint64_t* kb = a.kbits + (size_t)t * H * WW;
+    // pixels past W (the last word) are not pixels: their dilated bits stay 0
+    const uint64_t vmask = (wi == WW - 1 && (W & 63)) ? (1ull << (W & 63)) - 1ull : ~0ull;
     uint64_t out[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) out[i] = 0;
@@ -658,13 +667,18 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
         uint64_t o = c;
         for (int off = 1; off <= k - 1 - an; ++off) o |= (c >> off) | (nv << (64 - off));
         for (int off = 1; off <= an; ++off) o |= (c << off) | (pv >> (64 - off));
+        o &= vmask;
 #pragma unroll
         for (int i = 0; i < B; ++i)
             if (r - i >= 0 && r - i < k) out[i] |= o;
     }
+#pragma unroll
+    for (int i = 0; i < B; ++i)   // rows past H (a partial last block row) are not pixels
+        if (y0 + i >= H) out[i] = 0;
     if (a.dbg_dil && t == a.n - 1) {
 #pragma unroll
-        for (int i = 0; i < B; ++i) a.dbg_dil[(size_t)(y0 + i) * WW + wi] = out[i];
+        for (int i = 0; i < B; ++i)
+            if (y0 + i < H) a.dbg_dil[(size_t)(y0 + i) * WW + wi] = out[i];
     }
     BT* db = reinterpret_cast<BT*>(a.dblk) + (size_t)t * NBY * NBX + (size_t)by * NBX;
     constexpr int PER = 64 / B;
@@ -687,7 +701,7 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     typedef typename BlkT<B>::T BT;
     constexpr BT ROWM = (BT)((1u << B) - 1);
     const int lane = threadIdx.x;
-    const int W = a.g.W, H = a.g.H, NBX = W / B, NBY = H / B;
+    const int NBX = a.NBX, NBY = a.NBY, AP = a.ap;   // acc padded to NBX*B x NBY*B: partial blocks' pad stays 0
     const int bxi = blockIdx.x * 64 + lane, by = blockIdx.y;
     const bool active = bxi < NBX;
     const int bxc = min(bxi, NBX - 1);
@@ -696,7 +710,7 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     uint32_t acv[B][B / 4];
 #pragma unroll
     for (int i = 0; i < B; ++i) {
-        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(y0 + i) * W + x0);
+        const uint32_t* ac = reinterpret_cast<const uint32_t*>(a.acc + (size_t)(y0 + i) * AP + x0);
 #pragma unroll
         for (int d = 0; d < B / 4; ++d) acv[i][d] = ac[d];
     }
@@ -774,7 +788,7 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     if (active) {
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(y0 + i) * W + x0);
+            uint32_t* ac = reinterpret_cast<uint32_t*>(a.acc + (size_t)(y0 + i) * AP + x0);
 #pragma unroll
             for (int d = 0; d < B / 4; ++d) ac[d] = acv[i][d];
         }
@@ -782,14 +796,29 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     if (lane == 0 && nstatic) atomicAdd(a.stats + STAT_SLOT(blockIdx.x * 7 + blockIdx.y) * 4 + 3, nstatic);
 }
 
+// ND dwords to a row of an output frame: dword stores, or byte stores when the
+// output layout is not 4-byte aligned (W % 4 != 0 and dense output rows)
+template <int ND>
+__device__ __forceinline__ void store_row(uint8_t* dst, const uint32_t* w, int bytes)
+{
+    if (!bytes) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) o[d] = w[d];
+    } else {
+#pragma unroll
+        for (int d = 0; d < 4 * ND; ++d) dst[d] = (uint8_t)(w[d >> 2] >> (8 * (d & 3)));
+    }
+}
+
 // k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
-// row, one lane per BxB block, of frame t of the batch.
+// row, one lane per full BxB block, of frame t of the batch.
 template <int B>
 __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int ty, int lane, int wave)
 {
     const int W = a.g.W, H = a.g.H;
     const int bx = tx * 64 * B + lane * B, by = (ty * 4 + wave) * B;
-    if (bx >= W || by >= H) return;
+    if (bx + B > W || by + B > H) return;   // partial edge blocks: k_out_gen
     const uint8_t* f = a.bgr + (size_t)t * a.fstride;
     uint32_t px[B][3 * B / 4];
 #pragma unroll
@@ -803,8 +832,8 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
     // overlay (fd:110-111): (0,0,255) where acc > 127
     if (a.overlay) {
         typedef typename BlkT<B>::T BT;
-        const int NBX = W / B;
-        const BT rf = reinterpret_cast<const BT*>(a.rblk)[(size_t)t * (H / B) * NBX + (size_t)(by / B) * NBX + bx / B];
+        const int NBX = a.NBX;
+        const BT rf = reinterpret_cast<const BT*>(a.rblk)[(size_t)t * a.NBY * NBX + (size_t)(by / B) * NBX + bx / B];
         uint32_t red[B];
         const bool rany = rf != 0;
 #pragma unroll
@@ -832,9 +861,7 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
                 for (int d = 0; d < 3 * B / 4; ++d)
                     ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
             }
-            uint32_t* o = reinterpret_cast<uint32_t*>(ovf + (size_t)(by + i) * a.opitch + 3 * bx);
-#pragma unroll
-            for (int d = 0; d < 3 * B / 4; ++d) o[d] = ow[d];
+            store_row<3 * B / 4>(ovf + (size_t)(by + i) * a.opitch + 3 * bx, ow, a.obytes);
         }
     }
     // compressed (fd:115-130): BGR -> YCrCb; static block: Y' = trunc(clip(IDCT(
@@ -890,9 +917,7 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
         }
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            uint32_t* o = reinterpret_cast<uint32_t*>(cpf + (size_t)(by + i) * a.opitch + 3 * bx);
-#pragma unroll
-            for (int d = 0; d < 3 * B / 4; ++d) o[d] = cw[i][d];
+            store_row<3 * B / 4>(cpf + (size_t)(by + i) * a.opitch + 3 * bx, cw[i], a.obytes);
         }
     }
 }
@@ -911,19 +936,292 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a, int ntx, int nty)
     }
 }
 
+// ------------------------------------------------------------- resize ------
+// cv2.resize(frame, (W, H)) of 8UC3 with INTER_LINEAR (fd:74, fd:91), one lane
+// per output pixel (3 bytes): exact 2x down = OpenCV's INTER_AREA fast path,
+// (a + b + c + d + 2) >> 2; otherwise the fixed-point linear path with the
+// host-built tables (resize_tables): horizontal products exact in int32, the
+// vertical combination with OpenCV's 128-bit SIMD rounding for the first
+// simd_end bytes of a row and the scalar FixedPtCast after them.
+__global__ void __launch_bounds__(256) k_resize(const uint8_t* __restrict__ src, int spitch, size_t sstride,
+                                                uint8_t* __restrict__ dst, int dpitch, size_t dstride, ResizeTab rt)
+{
+    const int dx = blockIdx.x * 256 + threadIdx.x, dy = blockIdx.y, t = blockIdx.z;
+    if (dx >= rt.dw) return;
+    const uint8_t* f = src + (size_t)t * sstride;
+    uint8_t* o = dst + (size_t)t * dstride + (size_t)dy * dpitch + 3 * dx;
+    if (rt.area2x) {
+        const uint8_t* r0 = f + (size_t)(2 * dy) * spitch + 6 * dx;
+        const uint8_t* r1 = r0 + spitch;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = (uint8_t)((r0[c] + r0[c + 3] + r1[c] + r1[c + 3] + 2) >> 2);
+        return;
+    }
+    const int sx = rt.xo[3 * dx], a0 = rt.xo[3 * dx + 1], a1 = rt.xo[3 * dx + 2];
+    const int sy = rt.yo[3 * dy], b0 = rt.yo[3 * dy + 1], b1 = rt.yo[3 * dy + 2];
+    const int sx1 = sx + 1 < rt.sw ? sx + 1 : sx, sy1 = sy + 1 < rt.sh ? sy + 1 : sy;
+    const uint8_t* r0 = f + (size_t)sy * spitch;
+    const uint8_t* r1 = f + (size_t)sy1 * spitch;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int S0 = r0[3 * sx + c] * a0 + r0[3 * sx1 + c] * a1;
+        const int S1 = r1[3 * sx + c] * a0 + r1[3 * sx1 + c] * a1;
+        int v;
+        if (3 * dx + c < rt.simd_end)
+            v = ((((S0 >> 4) * b0) >> 16) + (((S1 >> 4) * b1) >> 16) + 2) >> 2;
+        else
+            v = (int)(((long long)S0 * b0 + (long long)S1 * b1 + (1 << 21)) >> 22);
+        o[c] = (uint8_t)satu8(v);
+    }
+}
+
+// ------------------------------------------------------ generic back end ----
+// Any block size (and the partial edge blocks of B = 4, 8): row-major bit
+// planes instead of block fields.
+//   k_dilate_rows  one lane per (64-px word, row): k x k dilation (fd:106)
+//   k_acc_rows     one lane per pixel, frames in order: addWeighted (fd:107)
+//                  -> acc > 127 (rbits) and acc != 0 (zbits) per frame
+//   k_out_gen      a workgroup per rectangle of blocks: overlay (fd:110-111),
+//                  static test (fd:120), block DCT / quantise / IDCT of any
+//                  block shape through LDS (fd:121-127), YCrCb round trip
+__global__ void __launch_bounds__(256) k_dilate_rows(BackArgs a)
+{
+    const int W = a.g.W, H = a.g.H, WW = a.g.WW;
+    const int idx = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y;
+    if (idx >= WW * H) return;
+    const int wi = idx % WW, y = idx / WW;
+    const int k = a.ksize, an = a.anchor;
+    const uint64_t* kb = a.kbits + (size_t)t * H * WW;
+    const uint64_t vmask = (wi == WW - 1 && (W & 63)) ? (1ull << (W & 63)) - 1ull : ~0ull;
+    uint64_t out = 0;
+    for (int r = 0; r < k; ++r) {
+        const int yy = y - an + r;
+        if (yy < 0 || yy >= H) continue;
+        const uint64_t* row = kb + (size_t)yy * WW;
+        const uint64_t c = row[wi], pv = wi > 0 ? row[wi - 1] : 0ull, nv = wi + 1 < WW ? row[wi + 1] : 0ull;
+        uint64_t o = c;
+        for (int off = 1; off <= k - 1 - an; ++off) o |= (c >> off) | (nv << (64 - off));
+        for (int off = 1; off <= an; ++off) o |= (c << off) | (pv >> (64 - off));
+        out |= o;
+    }
+    out &= vmask;
+    a.dbits[(size_t)t * H * WW + (size_t)y * WW + wi] = out;
+    if (a.dbg_dil && t == a.n - 1) a.dbg_dil[(size_t)y * WW + wi] = out;
+}
+
+__global__ void __launch_bounds__(64) k_acc_rows(BackArgs a)
+{
+    const int lane = threadIdx.x, wi = blockIdx.x, y = blockIdx.y;
+    const int W = a.g.W, H = a.g.H, WW = a.g.WW;
+    const int x = wi * 64 + lane;
+    const bool active = x < W;
+    uint8_t* ap = a.acc + (size_t)y * a.ap + (active ? x : 0);
+    uint32_t acc = active ? *ap : 0u;
+    const size_t plane = (size_t)H * WW, off = (size_t)y * WW + wi;
+    const float dil0 = __builtin_fmaf(0.f, a.beta, a.gamma), dil1 = __builtin_fmaf(255.f, a.beta, a.gamma);
+    constexpr int U = 8;
+    uint64_t dA[U], dB[U];
+    auto load_chunk = [&](int t0, uint64_t (&dst)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[u] = a.dbits[(size_t)min(t0 + u, a.n - 1) * plane + off];
+    };
+    auto frame = [&](int t, uint64_t d) {
+        const float tv = __builtin_fmaf((float)acc, a.alpha, ((d >> lane) & 1ull) ? dil1 : dil0);
+        acc = (uint32_t)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(tv), 0.f), 255.f);
+        const uint64_t r = __ballot(active && acc > 127u), z = __ballot(active && acc != 0u);
+        if (lane == 0) {
+            a.rbits[(size_t)t * plane + off] = r;
+            a.zbits[(size_t)t * plane + off] = z;
+        }
+    };
+    load_chunk(0, dA);
+    for (int t0 = 0; t0 < a.n; t0 += 2 * U) {
+        load_chunk(t0 + U, dB);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + u < a.n) frame(t0 + u, dA[u]);
+        load_chunk(t0 + 2 * U, dA);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t0 + U + u < a.n) frame(t0 + U + u, dB[u]);
+    }
+    if (active) *ap = (uint8_t)acc;
+}
+
+// A rectangle of blocks of one frame: the region [rx0, rx1) x [ry0, ry1) cut
+// into jobs of jbx x jby blocks (njx jobs across), one workgroup each.
+struct GenRegion {
+    int rx0, rx1, ry0, ry1;
+    int jbx, jby, njx;
+};
+
+__device__ __forceinline__ int luma_px(int b, int g, int r) { return descale14(b * 1868 + g * 9617 + r * 4899); }
+
+__global__ void __launch_bounds__(256) k_out_gen(BackArgs a, GenRegion R, int fast)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds_g[];
+    const int t = blockIdx.y, tid = threadIdx.x;
+    const int B = a.B, W = a.g.W, H = a.g.H, WW = a.g.WW;
+    const int jx = blockIdx.x % R.njx, jy = blockIdx.x / R.njx;
+    const int bx0 = R.rx0 + jx * R.jbx, bx1 = min(R.rx1, bx0 + R.jbx);
+    const int by0 = R.ry0 + jy * R.jby, by1 = min(R.ry1, by0 + R.jby);
+    if (bx0 >= bx1 || by0 >= by1) return;
+    const int px0 = bx0 * B, py0 = by0 * B;
+    const int JW = min(W, bx1 * B) - px0, JH = min(H, by1 * B) - py0;
+    const int nbx = bx1 - bx0, nblk = nbx * (by1 - by0), npx = JW * JH;
+    const int cap = R.jbx * R.jby * B * B;
+    float* X = lds_g;
+    float* T = X + cap;
+    int* flag = reinterpret_cast<int*>(T + cap);   // per block: 0 moving, 1 static, 2 static with an odd side
+    const int bwp = W % B, bhp = H % B;
+    const float* MB = a.Mtab;
+    const float* MWp = a.Mtab + B * B;
+    const float* MHp = MWp + bwp * bwp;
+    const size_t plane = (size_t)H * WW;
+    const uint8_t* f = a.bgr + (size_t)t * a.fstride;
+
+    // static test per block (fd:120)
+    int nst = 0;
+    for (int b = tid; b < nblk; b += 256) {
+        const int gbx = bx0 + b % nbx, gby = by0 + b / nbx;
+        const int bw = min(B, W - gbx * B), bh = min(B, H - gby * B);
+        bool st;
+        if (fast) {
+            st = (a.sbits[(size_t)t * a.sstride + (size_t)gby * a.SW + (gbx >> 6)] >> (gbx & 63)) & 1ull;
+        } else {
+            st = true;
+            const uint64_t* zb = a.zbits + (size_t)t * plane;
+            for (int i = 0; i < bh && st; ++i) {
+                const int ya = gby * B + i, s0 = gbx * B, e0 = s0 + bw - 1;
+                for (int w = s0 >> 6; w <= (e0 >> 6); ++w) {
+                    uint64_t m = ~0ull;
+                    if (w == (s0 >> 6)) m &= ~0ull << (s0 & 63);
+                    if (w == (e0 >> 6)) m &= ~0ull >> (63 - (e0 & 63));
+                    if (zb[(size_t)ya * WW + w] & m) { st = false; break; }
+                }
+            }
+        }
+        int fl = st ? 1 : 0;
+        if (st && ((bw > 1 && (bw & 1)) || (bh > 1 && (bh & 1)))) {   // cv2.dct raises (fd:122)
+            fl = 2;
+            atomicMin(a.err, a.frame0 + (unsigned long long)t);
+        }
+        nst += st;
+        flag[b] = fl;
+    }
+    if (!fast) {
+        for (int d = 32; d >= 1; d >>= 1) nst += __shfl_xor(nst, d, 64);
+        if ((tid & 63) == 0 && nst) atomicAdd(a.stats + STAT_SLOT(blockIdx.x + 5 * t) * 4 + 3, (unsigned long long)nst);
+    }
+    __syncthreads();
+
+    // overlay, Y - 128 of static blocks into LDS, round trip of the rest
+    for (int e = tid; e < npx; e += 256) {
+        const int i = e / JW, j = e - i * JW, y = py0 + i, x = px0 + j;
+        const int b = (i / B) * nbx + j / B;
+        const uint8_t* px = f + (size_t)y * a.pitch + 3 * x;
+        const int cb = px[0], cg = px[1], cr = px[2];
+        if (a.overlay) {
+            bool red;
+            if (fast) {
+                const size_t fi = (size_t)t * a.NBY * a.NBX + (size_t)(y / B) * a.NBX + x / B;
+                const int bit = (y % B) * B + x % B;
+                red = B == 4 ? (reinterpret_cast<const uint16_t*>(a.rblk)[fi] >> bit) & 1
+                             : (reinterpret_cast<const uint64_t*>(a.rblk)[fi] >> bit) & 1ull;
+            } else {
+                red = (a.rbits[(size_t)t * plane + (size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
+            }
+            uint8_t* o = a.overlay + (size_t)t * a.ostride + (size_t)y * a.opitch + 3 * x;
+            o[0] = red ? 0 : (uint8_t)cb;
+            o[1] = red ? 0 : (uint8_t)cg;
+            o[2] = red ? 255 : (uint8_t)cr;
+        }
+        const int yv = luma_px(cb, cg, cr);
+        if (flag[b] == 1) {
+            X[e] = (float)(yv - 128);
+        } else if (a.compressed) {
+            const int crv = (int)satu8(descale14((cr - yv) * 11682 + (128 << 14))) - 128;
+            const int cbv = (int)satu8(descale14((cb - yv) * 9241 + (128 << 14))) - 128;
+            uint8_t* o = a.compressed + (size_t)t * a.ostride + (size_t)y * a.opitch + 3 * x;
+            o[0] = (uint8_t)satu8(yv + descale14(cbv * 29049));
+            o[1] = (uint8_t)satu8(yv + descale14(cbv * -5636 + crv * -11698));
+            o[2] = (uint8_t)satu8(yv + descale14(crv * 22987));
+        }
+    }
+    __syncthreads();
+    // the separable DCT passes of every static block (the oracle's fmaf chains,
+    // oc_dct2d_rect / oc_idct2d_rect), one output element per lane
+    auto geom = [&](int e, int& i, int& j, int& b, int& bw, int& bh, const float*& Mw, const float*& Mh) {
+        i = e / JW;
+        j = e - i * JW;
+        b = (i / B) * nbx + j / B;
+        bw = min(B, W - (px0 + j - j % B));
+        bh = min(B, H - (py0 + i - i % B));
+        Mw = bw == B ? MB : MWp;
+        Mh = bh == B ? MB : MHp;
+    };
+    for (int e = tid; e < npx; e += 256) {          // rows: T[i][k] = sum_n X[i][n] Mw[k][n]
+        int i, j, b, bw, bh;
+        const float *Mw, *Mh;
+        geom(e, i, j, b, bw, bh, Mw, Mh);
+        if (flag[b] != 1) continue;
+        const int k = j % B, xs = i * JW + j - k;
+        float v = X[xs] * Mw[k * bw];
+        for (int n = 1; n < bw; ++n) v = __builtin_fmaf(X[xs + n], Mw[k * bw + n], v);
+        T[e] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < npx; e += 256) {          // cols + quantise: rint(sum_i Mh[k][i] T[i][l] / q) q
+        int i, j, b, bw, bh;
+        const float *Mw, *Mh;
+        geom(e, i, j, b, bw, bh, Mw, Mh);
+        if (flag[b] != 1) continue;
+        const int k = i % B, ys = (i - k) * JW + j;
+        float v = Mh[k * bh] * T[ys];
+        for (int r = 1; r < bh; ++r) v = __builtin_fmaf(Mh[k * bh + r], T[ys + r * JW], v);
+        X[e] = __builtin_rintf(div_rn(v, a.qinv)) * a.quant;
+    }
+    __syncthreads();
+    for (int e = tid; e < npx; e += 256) {          // inverse rows: T[k][n] = sum_l Y[k][l] Mw[l][n]
+        int i, j, b, bw, bh;
+        const float *Mw, *Mh;
+        geom(e, i, j, b, bw, bh, Mw, Mh);
+        if (flag[b] != 1) continue;
+        const int nn = j % B, xs = i * JW + j - nn;
+        float v = X[xs] * Mw[nn];
+        for (int l = 1; l < bw; ++l) v = __builtin_fmaf(X[xs + l], Mw[l * bw + nn], v);
+        T[e] = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < npx; e += 256) {          // inverse cols, +128, clip, truncate; (Y', Y', Y')
+        int i, j, b, bw, bh;
+        const float *Mw, *Mh;
+        geom(e, i, j, b, bw, bh, Mw, Mh);
+        if (flag[b] != 1 || !a.compressed) continue;
+        const int ii = i % B, ys = (i - ii) * JW + j;
+        float v = Mh[ii] * T[ys];
+        for (int r = 1; r < bh; ++r) v = __builtin_fmaf(Mh[r * bh + ii], T[ys + r * JW], v);
+        const uint8_t g = (uint8_t)(uint32_t)__builtin_amdgcn_fmed3f(v + 128.0f, 0.0f, 255.0f);
+        uint8_t* o = a.compressed + (size_t)t * a.ostride + (size_t)(py0 + i) * a.opitch + 3 * (px0 + j);
+        o[0] = g;
+        o[1] = g;
+        o[2] = g;
+    }
+}
+
 // --------------------------------------------------------------- launchers --
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
-                        int W, int H, const GaussTaps& k, hipStream_t s)
+                        int W, int H, int gs, const GaussTaps& k, hipStream_t s)
 {
-    dim3 gq((W / 4 + 255) / 256, H), gp((W + 255) / 256, H);
-    hipLaunchKernelGGL(k_gray, gq, dim3(256), 0, s, bgr, pitch, gray_tmp, W, H);
-    hipLaunchKernelGGL(k_hblur_q8, gp, dim3(256), 0, s, gray_tmp, tmp32, W, H, k);
-    hipLaunchKernelGGL(k_vblur_q8, gp, dim3(256), 0, s, tmp32, out, W, H, k);
+    dim3 gq((gs / 4 + 255) / 256, H), gp((W + 255) / 256, H);
+    hipLaunchKernelGGL(k_gray, gq, dim3(256), 0, s, bgr, pitch, gray_tmp, W, H, gs);
+    hipLaunchKernelGGL(k_hblur_q8, gp, dim3(256), 0, s, gray_tmp, tmp32, W, H, gs, k);
+    hipLaunchKernelGGL(k_vblur_q8, gp, dim3(256), 0, s, tmp32, out, W, H, gs, k);
     return hipGetLastError();
 }
 
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
-                        uint8_t* gray_out, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
+                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
     // chunks: ~1280 workgroups, at least 8 frames per chunk (1080p x 191: 2
@@ -937,7 +1235,49 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, co
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(k_front, dim3(tx, ty, chunks), dim3(256), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
-                       gray_out, mbits, g.W, g.H, g.WW, ithresh);
+                       gray_out, gs, mbits, g.W, g.H, g.WW, ithresh);
+    return hipGetLastError();
+}
+
+// resizeGeneric_'s coefficient tables (OpenCV 4.11 resize.cpp, INTER_LINEAR,
+// fixed point for 8U): fx = (float)((d + 0.5) * scale - 0.5), s = floor(fx),
+// fx -= s, clamped at the borders; coefficients cvRound((1 - fx) * 2048) and
+// cvRound(fx * 2048). Same restatement as oracle/dvc_oracle.c oc_linear_tab.
+static void linear_tab(int ssize, int dsize, int* tab)
+{
+    const double inv = (double)dsize / ssize, scale = 1. / inv;
+    for (int d = 0; d < dsize; ++d) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int sx = (int)std::floor(f);
+        f -= (float)sx;
+        if (sx < 0) { f = 0.f; sx = 0; }
+        if (sx >= ssize - 1) { f = 0.f; sx = ssize - 1; }
+        tab[3 * d] = sx;
+        tab[3 * d + 1] = std::max(-32768, std::min(32767, (int)std::nearbyint((1.f - f) * 2048.f)));
+        tab[3 * d + 2] = std::max(-32768, std::min(32767, (int)std::nearbyint(f * 2048.f)));
+    }
+}
+
+void resize_tables(int sw, int sh, int dw, int dh, int* host_x, int* host_y, int* area2x, int* simd_end)
+{
+    const double scx = 1. / ((double)dw / sw), scy = 1. / ((double)dh / sh);
+    *area2x = std::fabs(scx - 2.0) < 2.220446049250313e-16 && std::fabs(scy - 2.0) < 2.220446049250313e-16;
+    linear_tab(sw, dw, host_x);
+    linear_tab(sh, dh, host_y);
+    // VResizeLinearVec_32s8u (128-bit): 16-byte steps while x <= w - 16, then
+    // 8-byte steps while x < w - 8; the scalar loop does the rest
+    const int w = 3 * dw;
+    int x = 0;
+    while (x <= w - 16) x += 16;
+    while (x < w - 8) x += 8;
+    *simd_end = x;
+}
+
+hipError_t launch_resize(const uint8_t* src, int spitch, size_t sstride, uint8_t* dst, int dpitch, size_t dstride,
+                         int n, const ResizeTab& t, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_resize, dim3((t.dw + 255) / 256, t.dh, n), dim3(256), 0, s, src, spitch, sstride, dst, dpitch,
+                       dstride, t);
     return hipGetLastError();
 }
 
@@ -975,20 +1315,46 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
 template <int B>
 static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
 {
-    const int NBY = a.g.H / B;
-    hipLaunchKernelGGL(k_dilate<B>, dim3((a.g.WW * NBY + 255) / 256, a.n), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_acc<B>, dim3(a.SW, NBY), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_dilate<B>, dim3((a.g.WW * a.NBY + 255) / 256, a.n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_acc<B>, dim3(a.SW, a.NBY), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_accumulate(const BackArgs& a, int block, hipStream_t s)
+hipError_t launch_accumulate(const BackArgs& a, hipStream_t s)
 {
-    return block == 4 ? launch_acc<4>(a, s) : launch_acc<8>(a, s);
+    if (a.B == 4) return launch_acc<4>(a, s);
+    if (a.B == 8) return launch_acc<8>(a, s);
+    hipLaunchKernelGGL(k_dilate_rows, dim3((a.g.WW * a.g.H + 255) / 256, a.n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_acc_rows, dim3(a.g.WW, a.g.H), dim3(64), 0, s, a);
+    return hipGetLastError();
 }
 
-hipError_t launch_out(const BackArgs& a, int block, hipStream_t s)
+// k_out_gen over a region, jobs of about 1024 px (at least one block)
+static void launch_gen(const BackArgs& a, int rx0, int rx1, int ry0, int ry1, int jbx, int jby, int fast, hipStream_t s)
 {
-    if (!a.overlay && !a.compressed) return hipSuccess;
+    if (rx0 >= rx1 || ry0 >= ry1) return;
+    GenRegion R{rx0, rx1, ry0, ry1, std::max(1, std::min(jbx, rx1 - rx0)), std::max(1, std::min(jby, ry1 - ry0)), 0};
+    R.njx = (rx1 - rx0 + R.jbx - 1) / R.jbx;
+    const int njy = (ry1 - ry0 + R.jby - 1) / R.jby;
+    const size_t lds = (size_t)8 * R.jbx * R.jby * a.B * a.B + (size_t)4 * R.jbx * R.jby;
+    hipLaunchKernelGGL(k_out_gen, dim3(R.njx * njy, a.n), dim3(256), lds, s, a, R, fast);
+}
+
+hipError_t launch_out(const BackArgs& a, hipStream_t s)
+{
+    const int B = a.B;
+    const int per = std::max(1, 1024 / (B * B));             // blocks of a ~1024-px job
+    if (!fast_block(B)) {
+        int jb = 1;
+        while ((jb + 1) * (jb + 1) <= per) ++jb;
+        launch_gen(a, 0, a.NBX, 0, a.NBY, jb, jb, 0, s);
+        return hipGetLastError();
+    }
+    // partial edge blocks (right column, bottom row) of the fast layout
+    const bool pw = a.g.W % B, ph = a.g.H % B;
+    if (pw) launch_gen(a, a.NBX - 1, a.NBX, 0, a.NBY, 1, per, 1, s);
+    if (ph) launch_gen(a, 0, a.NBX - (pw ? 1 : 0), a.NBY - 1, a.NBY, per, 1, 1, s);
+    if (!a.overlay && !a.compressed) return hipGetLastError();
     // 128 workgroups per CU (32768 on MI355X): measured best of 8k..64k beside
     // the CCL chain at 1080p x 191 (+1 % over 64/CU); DVC_OUT_WGS overrides
     static const int wgs = [] {
@@ -997,9 +1363,9 @@ hipError_t launch_out(const BackArgs& a, int block, hipStream_t s)
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
         return 128 * cus;
     }();
-    const int ntx = (a.g.W + 64 * block - 1) / (64 * block), nty = (a.g.H + 4 * block - 1) / (4 * block);
+    const int ntx = (a.g.W + 64 * B - 1) / (64 * B), nty = (a.g.H + 4 * B - 1) / (4 * B);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
-    if (block == 4) hipLaunchKernelGGL(k_out<4>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    if (B == 4) hipLaunchKernelGGL(k_out<4>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
     else hipLaunchKernelGGL(k_out<8>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
     return hipGetLastError();
 }

@@ -21,7 +21,8 @@ from . import _native as N
 
 def derive_params(width: int, height: int, block_size: int = 4, motion_threshold: float = 0.5,
                   min_area: float = 500, kernel_size: int = 7, release_factor: float = 0.5,
-                  quantization_level: float = 100, flags: int = 0) -> N.FdParams:
+                  quantization_level: float = 100, flags: int = 0, src_width: int = 0,
+                  src_height: int = 0) -> N.FdParams:
     """dvc_fd_params from the reference kwargs (frame_differencing.py:21-30).
 
     * ``ithresh = floor(motion_threshold)`` clamped to [-1, 255]: cv::threshold
@@ -45,6 +46,7 @@ def derive_params(width: int, height: int, block_size: int = 4, motion_threshold
     p.prime_ksize = 25   # fd:77
     p.prime_sigma = 30.0
     p.flags = flags
+    p.src_width, p.src_height = int(src_width or 0), int(src_height or 0)
     return p
 
 
@@ -52,7 +54,10 @@ class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
                  device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
                  max_batch: int = 1, **kwargs):
-        """``max_batch``: frames one device launch covers in :meth:`step_batch`
+        """``width, height``: the scaled frame size (fd:60-61); frames handed to
+        :meth:`prime`/:meth:`step` are ``src_width x src_height`` (the video's,
+        default the same) and are resized on the GPU (fd:74,91).
+        ``max_batch``: frames one device launch covers in :meth:`step_batch`
         (the contour-filter scratch is sized for NSLOT = 3 batches of max_batch
         frames in flight, fd_api.hip). ``stream``: the caller's HIP stream
         (``torch.cuda.Stream.cuda_stream``), joined as dvc_fd_create documents."""
@@ -61,6 +66,8 @@ class FDWorker:
         self.params = derive_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
+        self.SW = int(kwargs.get("src_width") or width)
+        self.SH = int(kwargs.get("src_height") or height)
         self.device = int(device)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
@@ -72,6 +79,12 @@ class FDWorker:
     # -------------------------------------------------------------- frames --
     @property
     def _fshape(self):
+        """Input frames (source size)."""
+        return (self.SH, self.SW, 3)
+
+    @property
+    def _oshape(self):
+        """Output frames (scaled size)."""
         return (self.H, self.W, 3)
 
     def _dev(self, x, name, n=None, batched=False, tail=None):
@@ -82,10 +95,10 @@ class FDWorker:
         """fd:67-81: previous gray := GaussianBlur(gray(frame), 25x25, 30); acc := 0."""
         if self.device_ptrs:
             addr, _ = self._dev(frame, "frame")
-            N.check(self._lib.dvc_fd_prime(self._h, addr, 3 * self.W))
+            N.check(self._lib.dvc_fd_prime(self._h, addr, 3 * self.SW))
         else:
             f = B.host_in(frame, self._fshape, "frame")
-            N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, 3 * self.W))
+            N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, 3 * self.SW))
 
     def step(self, frame, overlay=None, compressed=None, acc=None, want=("overlay", "compressed")):
         """fd:91-133 for one frame.
@@ -96,16 +109,16 @@ class FDWorker:
         """
         if self.device_ptrs:
             addr, _ = self._dev(frame, "frame")
-            ov = self._dev(overlay, "overlay")[0] if overlay is not None else None
-            cp = self._dev(compressed, "compressed")[0] if compressed is not None else None
+            ov = self._dev(overlay, "overlay", tail=self._oshape)[0] if overlay is not None else None
+            cp = self._dev(compressed, "compressed", tail=self._oshape)[0] if compressed is not None else None
             ac = self._dev(acc, "acc", tail=(self.H, self.W))[0] if acc is not None else None
-            N.check(self._lib.dvc_fd_step(self._h, addr, 3 * self.W, ov, cp, ac))
+            N.check(self._lib.dvc_fd_step(self._h, addr, 3 * self.SW, ov, cp, ac))
             return None
         f = B.host_in(frame, self._fshape, "frame")
-        overlay = B.host_out(overlay, self._fshape, "overlay", "overlay" in want)
-        compressed = B.host_out(compressed, self._fshape, "compressed", "compressed" in want)
+        overlay = B.host_out(overlay, self._oshape, "overlay", "overlay" in want)
+        compressed = B.host_out(compressed, self._oshape, "compressed", "compressed" in want)
         acc = B.host_out(acc, (self.H, self.W), "acc", False)
-        N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, 3 * self.W,
+        N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, 3 * self.SW,
                                       overlay.ctypes.data if overlay is not None else None,
                                       compressed.ctypes.data if compressed is not None else None,
                                       acc.ctypes.data if acc is not None else None))
@@ -121,22 +134,23 @@ class FDWorker:
         handle's device (outputs may hold more frames), or explicit
         ``(address, n)`` tuples of dense frames; asynchronous, returns None.
         """
-        fs = 3 * self.W * self.H
+        fs, os_ = 3 * self.SW * self.SH, 3 * self.W * self.H
         if self.device_ptrs:
             addr, n = self._dev(frames, "frames", batched=True)
-            ov = self._dev(overlay, "overlay", n=n, batched=True)[0] if overlay is not None else None
-            cp = self._dev(compressed, "compressed", n=n, batched=True)[0] if compressed is not None else None
-            N.check(self._lib.dvc_fd_step_batch(self._h, addr, 3 * self.W, fs, n, ov, cp, fs))
+            ov = self._dev(overlay, "overlay", n=n, batched=True, tail=self._oshape)[0] if overlay is not None else None
+            cp = self._dev(compressed, "compressed", n=n, batched=True, tail=self._oshape)[0] \
+                if compressed is not None else None
+            N.check(self._lib.dvc_fd_step_batch(self._h, addr, 3 * self.SW, fs, n, ov, cp, os_))
             return None
         if not isinstance(frames, np.ndarray) or frames.ndim != 4:
-            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
+            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.SH}, {self.SW}, 3)")
         n = int(frames.shape[0])
         f = B.host_in(frames, (n,) + self._fshape, "frames")
-        overlay = B.host_out(overlay, f.shape, "overlay", "overlay" in want)
-        compressed = B.host_out(compressed, f.shape, "compressed", "compressed" in want)
-        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, n,
+        overlay = B.host_out(overlay, (n,) + self._oshape, "overlay", "overlay" in want)
+        compressed = B.host_out(compressed, (n,) + self._oshape, "compressed", "compressed" in want)
+        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.SW, fs, n,
                                             overlay.ctypes.data if overlay is not None else None,
-                                            compressed.ctypes.data if compressed is not None else None, fs))
+                                            compressed.ctypes.data if compressed is not None else None, os_))
         return overlay, compressed
 
     # ------------------------------------------------------------- queries --

@@ -1,6 +1,6 @@
 """Drop-in for the reference's ``frame_differencing.py`` (FD path).
 
-Same public surface, same kwargs and defaults, same side effects:
+Public surface, kwargs, defaults and side effects are the reference's:
 
 * ``setup_logging(output_dir)``                      — ``frame_differencing.py:7-19``
 * ``filter_and_dilate_movements(video_path, ...)``   — ``frame_differencing.py:21-159``
@@ -10,10 +10,15 @@ Outputs go to ``<output_dir>/<video basename>/``: ``dilated_motion_mask_video``
 and ``compressed_final_video`` (mp4v through OpenCV when importable, else an
 ``.npy`` frame stream of the same basename), ``execution_times.txt`` in the
 reference's exact format, and ``processing.log``. Errors are logged and the
-functions return ``None``, as the reference does (``fd:40-42, 68-71, 140-145``).
+functions return ``None`` (``fd:40-42, 68-71, 140-145``).
 
-The per-frame work (``fd:91-133``) runs on the GPU through ``FDWorker`` — the
-HIP kernels in ``csrc/`` — never through a CPU fallback.
+The per-frame work (``fd:91-133``, resize included) runs on the GPU through
+``FDWorker`` — the HIP kernels in ``csrc/`` — never through a CPU fallback. The
+frames are read ahead ``DVC_READ_AHEAD`` (default 32) at a time into
+page-locked buffers and stepped with one ``dvc_fd_step_batch`` call per group
+(identical results to one call per frame, which the batch tests prove): the
+device runs the group as launches over tiles x frames and the host copies
+overlap with the computation, instead of a synchronous round trip per frame.
 """
 from __future__ import annotations
 
@@ -21,44 +26,55 @@ import logging
 import os
 import time
 
-import numpy as np
-
 from . import video_io
+from ._native import DVC_E_ODD_DCT, DvcError, pinned
 from .fd import FDWorker
+
+LOG_FORMAT = "%(asctime)s - %(levelname)s - %(message)s"
+READ_AHEAD = int(os.environ.get("DVC_READ_AHEAD", "32"))
 
 
 def setup_logging(output_dir):
-    """fd:7-19: processing.log + console; a no-op basicConfig if logging is set up."""
+    """fd:7-19: ``processing.log`` (truncated) plus the console. Like the
+    reference it relies on ``basicConfig``, so it is a no-op when the process
+    has configured logging already (e.g. the GUI's handler)."""
     os.makedirs(output_dir, exist_ok=True)
-    log_file = os.path.join(output_dir, "processing.log")
-    logging.basicConfig(level=logging.INFO,
-                        format="%(asctime)s - %(levelname)s - %(message)s",
-                        handlers=[logging.FileHandler(log_file, mode='w'),
-                                  logging.StreamHandler()])
-    logging.info(f"Logging configured. Log file saved in: {log_file}")
-
-
-def resize_frame(frame: np.ndarray, size) -> np.ndarray:
-    """cv2.resize(frame, (sw, sh)) with INTER_LINEAR (fd:74,91).
-
-    * dsize == ssize: OpenCV copies the frame (the GUI default scale 1.0).
-    * exact 2x downscale: OpenCV turns INTER_LINEAR into the fast INTER_AREA
-      path, ``(a + b + c + d + 2) >> 2`` per 2x2 block.
-    Other scale factors are not implemented and raise.
-    """
-    sw, sh = int(size[0]), int(size[1])
-    h, w = frame.shape[:2]
-    if (sw, sh) == (w, h):
-        return frame
-    if sw * 2 == w and sh * 2 == h:
-        f = frame.astype(np.uint16)
-        s = f[0::2, 0::2] + f[0::2, 1::2] + f[1::2, 0::2] + f[1::2, 1::2]
-        return ((s + 2) >> 2).astype(np.uint8)
-    raise NotImplementedError(f"scale to {sw}x{sh} from {w}x{h}: only 1.0 and exact 0.5 are implemented")
+    log_path = os.path.join(output_dir, "processing.log")
+    sinks = [logging.FileHandler(log_path, mode="w"), logging.StreamHandler()]
+    logging.basicConfig(level=logging.INFO, format=LOG_FORMAT, handlers=sinks)
+    logging.info(f"Logging configured. Log file saved in: {log_path}")
 
 
 def _device() -> int:
     return int(os.environ.get("DVC_DEVICE", os.environ.get("LOCAL_RANK", 0)))
+
+
+def _feed_dir(output_dir, video_path) -> str:
+    """<output_dir>/<basename without extension> (fd:45-46, fd:177-178)."""
+    return os.path.join(output_dir, video_io.video_name(video_path))
+
+
+class _Writers:
+    """The two mp4v outputs of fd:63-65 plus the progress callback of fd:137-138."""
+
+    def __init__(self, out_dir, fps, size, progress_callback):
+        self.mask = video_io.open_sink(os.path.join(out_dir, "dilated_motion_mask_video.mp4"), fps, size)
+        self.final = video_io.open_sink(os.path.join(out_dir, "compressed_final_video.mp4"), fps, size)
+        self.callback = progress_callback
+        self.frames = 0
+
+    def emit(self, overlay, compressed):
+        self.mask.write(overlay)
+        if compressed is None:       # the frame whose block loop raised: overlay only (fd:112 < fd:122)
+            return
+        self.final.write(compressed)
+        self.frames += 1
+        if self.callback is not None and self.frames % 50 == 0:
+            self.callback(self.frames)
+
+    def release(self):
+        self.mask.release()
+        self.final.release()
 
 
 def filter_and_dilate_movements(video_path, output_dir,
@@ -72,85 +88,91 @@ def filter_and_dilate_movements(video_path, output_dir,
                                 scale_factor=1.0,
                                 progress_callback=None):
     """fd:21-159. ``search_area`` is accepted and unused, as in the reference."""
-    start_time = time.time()
+    t_start = time.time()
     cap = video_io.open_source(video_path)
     if not cap.isOpened():
         logging.error("Unable to open the video.")
         return
-
-    video_name = video_io.video_name(video_path)
-    video_output_dir = os.path.join(output_dir, video_name)
-    os.makedirs(video_output_dir, exist_ok=True)
-    setup_logging(video_output_dir)
-
-    mask_output_path = os.path.join(video_output_dir, "dilated_motion_mask_video.mp4")
-    final_output_path = os.path.join(video_output_dir, "compressed_final_video.mp4")
-    time_log_path = os.path.join(video_output_dir, "execution_times.txt")
+    out_dir = _feed_dir(output_dir, video_path)
+    os.makedirs(out_dir, exist_ok=True)
+    setup_logging(out_dir)
+    times_path = os.path.join(out_dir, "execution_times.txt")
 
     fps = int(cap.get(video_io.CAP_PROP_FPS))
-    width = int(cap.get(video_io.CAP_PROP_FRAME_WIDTH))
-    height = int(cap.get(video_io.CAP_PROP_FRAME_HEIGHT))
-    scaled_width = int(width * scale_factor)
-    scaled_height = int(height * scale_factor)
+    src_w = int(cap.get(video_io.CAP_PROP_FRAME_WIDTH))
+    src_h = int(cap.get(video_io.CAP_PROP_FRAME_HEIGHT))
+    out_w, out_h = int(src_w * scale_factor), int(src_h * scale_factor)   # fd:60-61
+    sinks = _Writers(out_dir, fps, (out_w, out_h), progress_callback)
 
-    mask_out = video_io.open_sink(mask_output_path, fps, (scaled_width, scaled_height))
-    final_out = video_io.open_sink(final_output_path, fps, (scaled_width, scaled_height))
-
-    ret, prev_frame = cap.read()
-    if not ret:
+    ok, first = cap.read()
+    if not ok:
         logging.error("Unable to read the first frame of the video.")
         cap.release()
         return
 
-    frame_count = 0
-    frame_processing_times = []
+    per_frame_s = []
     worker = None
     try:
-        prev_frame = resize_frame(prev_frame, (scaled_width, scaled_height))
-        worker = FDWorker(scaled_width, scaled_height, device=_device(),
+        R = max(1, READ_AHEAD)
+        worker = FDWorker(out_w, out_h, device=_device(), src_width=src_w, src_height=src_h, max_batch=R,
                           block_size=block_size, motion_threshold=motion_threshold, min_area=min_area,
                           kernel_size=kernel_size, release_factor=release_factor,
                           quantization_level=quantization_level)
-        worker.prime(prev_frame)
-        overlay = np.empty((scaled_height, scaled_width, 3), np.uint8)
-        compressed = np.empty_like(overlay)
-        while True:
-            frame_start = time.time()
-            ret, curr_frame = cap.read()
-            if not ret:
+        worker.prime(first)                                     # fd:67-81 (resize on the GPU)
+        frames = pinned((R, src_h, src_w, 3))
+        overlay, compressed = pinned((R, out_h, out_w, 3)), pinned((R, out_h, out_w, 3))
+        eof = False
+        while not eof:
+            t0 = time.time()
+            n = 0
+            while n < R:                                        # fd:87-89
+                ok, f = cap.read()
+                if not ok:
+                    eof = True
+                    break
+                frames[n] = f
+                n += 1
+            if n == 0:
                 break
-            curr_frame = resize_frame(curr_frame, (scaled_width, scaled_height))
-            worker.step(curr_frame, overlay, compressed)
-            mask_out.write(overlay)
-            final_out.write(compressed)
-            frame_count += 1
-            frame_processing_times.append(time.time() - frame_start)
-            if progress_callback is not None and frame_count % 50 == 0:
-                progress_callback(frame_count)
+            stop = None
+            try:                                                # fd:91-133, n times
+                worker.step_batch(frames[:n], overlay[:n], compressed[:n])
+                done = n
+            except DvcError as e:
+                if e.code != DVC_E_ODD_DCT:
+                    raise
+                stop, done = e, worker.stats()["frames"] - sinks.frames
+            for t in range(done):
+                sinks.emit(overlay[t], compressed[t])
+            per_frame_s.extend([(time.time() - t0) / n] * done)
+            if stop is not None:
+                sinks.emit(overlay[done], None)
+                raise RuntimeError("OpenCV(4.11.0) (-213:The function/feature is not implemented) "
+                                   "Odd-size DCT's are not implemented in function 'apply'") from stop
     except Exception as e:
         logging.error("Error during processing: " + str(e), exc_info=True)
     finally:
         cap.release()
-        mask_out.release()
-        final_out.release()
+        sinks.release()
         if worker is not None:
             worker.close()
 
-    total_time = time.time() - start_time
-    avg_time_per_frame = (sum(frame_processing_times) / len(frame_processing_times)
-                          if frame_processing_times else 0)
-    write_execution_times(time_log_path, frame_count, total_time, avg_time_per_frame)
-    logging.info(f"Execution statistics saved in: {time_log_path}")
+    total_time = time.time() - t_start
+    avg = sum(per_frame_s) / len(per_frame_s) if per_frame_s else 0
+    write_execution_times(times_path, sinks.frames, total_time, avg)
+    logging.info(f"Execution statistics saved in: {times_path}")
 
 
 def write_execution_times(path, frame_count, total_time, avg_time_per_frame):
     """fd:152-157, byte-identical layout (parsed by performance_analysis.py:44-109)."""
+    lines = ["Frame Differencing:",
+             f"  Frames processed: {frame_count}",
+             f"  Total time: {total_time:.2f} seconds",
+             f"  Average time per frame: {avg_time_per_frame:.4f} seconds",
+             "",
+             f"Total video processing time: {total_time:.2f} seconds"]
     with open(path, "w") as f:
-        f.write("Frame Differencing:\n")
-        f.write(f"  Frames processed: {frame_count}\n")
-        f.write(f"  Total time: {total_time:.2f} seconds\n")
-        f.write(f"  Average time per frame: {avg_time_per_frame:.4f} seconds\n\n")
-        f.write(f"Total video processing time: {total_time:.2f} seconds\n")
+        f.write("\n".join(lines) + "\n")
 
 
 def process_single_video_fd(video_path,
@@ -164,24 +186,16 @@ def process_single_video_fd(video_path,
                             quantization_level=100,
                             scale_factor=1.0,
                             progress_callback=None):
-    """fd:161-196."""
-    video_name = video_io.video_name(video_path)
-    video_output_dir = os.path.join(output_dir, video_name)
-    os.makedirs(video_output_dir, exist_ok=True)
-
-    setup_logging(video_output_dir)
-    logging.info(f"=== Start processing (Frame Differencing) for '{video_name}' ===")
-
-    filter_and_dilate_movements(video_path,
-                                output_dir,
-                                block_size=block_size,
-                                search_area=search_area,
-                                motion_threshold=motion_threshold,
-                                min_area=min_area,
-                                kernel_size=kernel_size,
-                                release_factor=release_factor,
-                                quantization_level=quantization_level,
-                                scale_factor=scale_factor,
-                                progress_callback=progress_callback)
-
-    logging.info(f"=== Processing successfully completed for '{video_name}'. ===")
+    """fd:161-196: the per-video entry point the GUI calls (windows.py:154) —
+    prepares the feed's folder and log, then runs the worker with every kwarg."""
+    options = dict(block_size=block_size, search_area=search_area, motion_threshold=motion_threshold,
+                   min_area=min_area, kernel_size=kernel_size, release_factor=release_factor,
+                   quantization_level=quantization_level, scale_factor=scale_factor,
+                   progress_callback=progress_callback)
+    name = video_io.video_name(video_path)
+    out_dir = _feed_dir(output_dir, video_path)
+    os.makedirs(out_dir, exist_ok=True)
+    setup_logging(out_dir)
+    logging.info(f"=== Start processing (Frame Differencing) for '{name}' ===")
+    filter_and_dilate_movements(video_path, output_dir, **options)
+    logging.info(f"=== Processing successfully completed for '{name}'. ===")

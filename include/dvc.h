@@ -13,17 +13,23 @@
  *
  * Conventions
  *  - Plain pointers and sizes only; no C++ or torch types cross this boundary.
- *  - Frames are packed 8-bit BGR, H rows of `pitch` bytes (pitch >= 3*W, and a
- *    multiple of 4), i.e. what cv2.VideoCapture.read() yields (fd:87).
+ *  - Frames are packed 8-bit BGR, H rows of `pitch` bytes (pitch >= 3*W), i.e.
+ *    what cv2.VideoCapture.read() yields (fd:87).
  *  - Every function returns DVC_OK (0) or a negative DVC_E_* status; the text of
  *    the last error on the calling thread is available from dvc_last_error().
  *    The Python host turns a negative status into logging.error(...) and an
  *    early return, mirroring the reference's try/except (fd:140-145).
  *  - A handle is single-threaded (one feed). Distinct handles may
  *    be driven from distinct host threads concurrently.
- *  - Unless DVC_FLAG_DEVICE_PTRS is set, frame/output pointers are host memory
- *    and are staged through pinned buffers owned by the handle; with the flag they
- *    are device pointers on the handle's device (device-resident benchmark mode).
+ *  - Unless DVC_FLAG_DEVICE_PTRS is set, frame/output pointers are host memory:
+ *    pageable buffers are staged through two sets of pinned buffers owned by
+ *    the handle (chunk c+1 goes up while chunk c computes and chunk c-1 comes
+ *    down), page-locked ones (dvc_host_alloc) are DMA'd directly; with the flag
+ *    they are device pointers on the handle's device (device-resident mode).
+ *  - Frame rows: `pitch` bytes each (>= 3*W), every row readable in full. Any
+ *    width and pitch are accepted; rows the kernels cannot read in place
+ *    (pitch % 4, rows shorter than 3*roundup(W,4) bytes) are re-pitched on
+ *    the device first.
  */
 #ifndef DVC_H
 #define DVC_H
@@ -35,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 3
+#define DVC_ABI_VERSION 4
 #define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
@@ -45,6 +51,10 @@ extern "C" {
 #define DVC_E_STATE       -3  /* call out of order (e.g. step before prime)    */
 #define DVC_E_NOMEM       -4  /* device or pinned allocation failed            */
 #define DVC_E_UNSUPPORTED -5  /* parameter combination not implemented on GPU */
+#define DVC_E_ODD_DCT     -6  /* a static block has an odd side > 1: cv2.dct
+                                 raises "Odd-size DCT's are not implemented"
+                                 (fd:122) and the reference loop stops
+                                 (fd:140); see dvc_fd_step                     */
 
 /* ---- flags ----------------------------------------------------------------- */
 #define DVC_FLAG_DEVICE_PTRS 0x1u /* prime/step pointers are device pointers   */
@@ -62,9 +72,14 @@ extern "C" {
 /*
  * Parameters, derived on the host from the reference kwargs of
  * filter_and_dilate_movements (fd:21-30):
- *   width,height  scaled frame size int(W*scale_factor), int(H*scale_factor) (fd:60-61);
- *                 frames handed to prime/step are already at this size.
- *   block         block_size (fd:22); the GPU supports 4 and 8.
+ *   width,height  scaled frame size int(W*scale_factor), int(H*scale_factor) (fd:60-61),
+ *                 any size >= 16 x 16.
+ *   src_width,src_height  size of the frames handed to prime/step (the
+ *                 video's, fd:57-58); 0 = width,height. When they differ the
+ *                 worker resizes every frame on the GPU first (cv2.resize
+ *                 INTER_LINEAR 8U, fd:74,91).
+ *   block         block_size (fd:22), 1..64; partial blocks at the right and
+ *                 bottom edges are their slices (fd:117-127).
  *   ithresh       floor(motion_threshold): cv::threshold on 8U floors the
  *                 threshold, so motion = absdiff > ithresh (fd:97).
  *   min_area2     floor(2*min_area): a contour is kept iff 2*area > min_area2,
@@ -95,8 +110,10 @@ typedef struct dvc_fd_params {
     uint32_t flags;
     uint32_t max_batch; /* 0/1..DVC_MAX_BATCH: frames one device launch covers in
                            dvc_fd_step_batch (longer calls are chunked). The
-                           contour-filter scratch (~18 MB per 1080p frame) is
-                           allocated for 2 x max_batch frames. */
+                           per-frame scratch is allocated for three batches in
+                           flight (3 x max_batch frames). */
+    int32_t src_width;  /* 0: = width  */
+    int32_t src_height; /* 0: = height */
 } dvc_fd_params;
 
 /* Cumulative per-handle counters (all frames stepped since create/prime). */
@@ -114,6 +131,13 @@ int         dvc_abi_version(void);
 const char* dvc_last_error(void);
 int         dvc_device_count(int* count);
 
+/* Page-locked host memory for frames and outputs: host-pointer steps DMA such
+ * buffers directly (no staging copy on the CPU). The reference's frames come
+ * from cv2.VideoCapture.read() (fd:87); a reader that decodes into these
+ * buffers feeds the worker at PCIe rate. */
+int  dvc_host_alloc(size_t bytes, void** out);
+void dvc_host_free(void* p);
+
 /* Create a feed handle on `device`. The stages run on four internal streams
  * (blur/threshold front, contour filter, dilate + accumulate, overlay/compress
  * output) with three batches' buffers in flight; only the two recurrences
@@ -128,8 +152,9 @@ int         dvc_device_count(int* count);
  * Replaces the per-video setup at fd:56-82. */
 int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc_fd** out);
 
-/* Frame 0: gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77) -> previous
- * gray; accumulated mask := 0 (fd:81). Resets the cumulative stats. */
+/* Frame 0: resize (fd:74), gray (fd:75) + GaussianBlur(25x25, sigma 30) (fd:77)
+ * -> previous gray; accumulated mask := 0 (fd:81). Resets the cumulative stats
+ * and clears a DVC_E_ODD_DCT stop. Frames are src_width x src_height. */
 int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch);
 
 /* One frame of the hot loop, fd:91-133: gray, GaussianBlur 5x5, absdiff,
@@ -142,7 +167,15 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch);
  *   acc_out     the accumulated mask after this frame, H*W bytes (fd:107)
  * The call is asynchronous with respect to the host when DVC_FLAG_DEVICE_PTRS
  * is set (dvc_fd_sync before reading outputs or reusing the input); with host
- * pointers it returns after the outputs have landed. */
+ * pointers it returns after the outputs have landed.
+ * DVC_E_ODD_DCT: the frame has a static block with an odd side > 1 (an odd
+ * block_size, or an odd partial edge block): like the reference, whose
+ * cv2.dct raises there (fd:122) and whose try/except ends the loop (fd:140),
+ * the frame's overlay is valid (fd:112 comes first), its compressed frame is
+ * not, it is not counted in the stats' `frames`, and the handle refuses
+ * further steps until the next prime. With device pointers the stop is
+ * detected on the device and reported by the next synchronising call
+ * (dvc_fd_sync / dvc_fd_get_stats / the next host-pointer step). */
 int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch,
                 uint8_t* overlay, uint8_t* compressed, uint8_t* acc_out);
 
@@ -154,7 +187,9 @@ int dvc_fd_step(dvc_fd* h, const uint8_t* bgr, size_t pitch,
  * accumulate / compress back walk the frames in order per tile (prev_gray and
  * the accumulated mask stay on chip), the contour filter of every frame of the
  * batch runs as one grid, and batch i+1's front overlaps batch i's back.
- * Same synchronisation rules as dvc_fd_step. */
+ * Same synchronisation rules as dvc_fd_step; on DVC_E_ODD_DCT the stats'
+ * `frames` counts the frames completed before the stopping one k (outputs
+ * before k are complete, overlay k is valid). */
 int dvc_fd_step_batch(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, int n,
                       uint8_t* overlay, uint8_t* compressed, size_t out_stride);
 
@@ -186,7 +221,7 @@ void dvc_fd_destroy(dvc_fd* h);
 /* The contour-area filter alone (fd:100-104) on an arbitrary host mask (H*W
  * bytes, nonzero = foreground): runs the same device kernels as dvc_fd_step
  * (run extraction, union-find, hole resolution, area, kept-mask paint) and
- * writes the filtered mask {0,255} to host memory. W, H multiples of 4.
+ * writes the filtered mask {0,255} to host memory. W, H >= 4.
  * *components (nullable) receives the number of external contours.
  * Synchronous; for the parity tests. */
 int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_area2,

@@ -46,6 +46,8 @@ class FdParams(ctypes.Structure):
         ("prime_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
         ("max_batch", ctypes.c_uint32),
+        ("src_width", ctypes.c_int32),
+        ("src_height", ctypes.c_int32),
     ]
 
 
@@ -97,6 +99,12 @@ def lib():
         fp = ctypes.POINTER(ctypes.c_float)
         L.oc_dct2d.argtypes = [fp, ctypes.c_int, fp, fp]
         L.oc_idct2d.argtypes = [fp, ctypes.c_int, fp, fp]
+        L.oc_dct2d_rect.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp]
+        L.oc_idct2d_rect.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp]
+        L.oc_dct_size_ok.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.oc_resize_simd_end.argtypes = [ctypes.c_int]
+        L.oc_resize_bgr.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t,
+                                    ctypes.c_int, ctypes.c_int]
         L.oc_block_quant.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                      ctypes.c_float, u8p, ctypes.c_int]
         L.oc_fd_create.argtypes = [ctypes.POINTER(FdParams), ctypes.c_int]
@@ -119,10 +127,12 @@ def _u8(a: np.ndarray):
 # ---------------------------------------------------------------- params ----
 def fd_params(width, height, block_size=4, motion_threshold=0.5, min_area=500,
               kernel_size=7, release_factor=0.5, quantization_level=100,
-              prime_ksize=25, prime_sigma=30.0) -> FdParams:
+              prime_ksize=25, prime_sigma=30.0, src_width=0, src_height=0) -> FdParams:
     """Host-side derivation of dvc_fd_params from the reference kwargs
-    (frame_differencing.py:21-30); same rules as the product's host code."""
+    (frame_differencing.py:21-30); same rules as the product's host code.
+    width/height are the scaled size (fd:60-61), src_* the video's (0: same)."""
     p = FdParams()
+    p.src_width, p.src_height = int(src_width), int(src_height)
     p.width, p.height, p.block = int(width), int(height), int(block_size)
     p.ithresh = max(-1, min(255, math.floor(motion_threshold)))
     p.min_area2 = math.floor(2.0 * float(min_area))
@@ -244,25 +254,47 @@ def dct_matrix(B: int) -> np.ndarray:
     return np.array(m[:], dtype=np.float32).reshape(B, B)
 
 
+class OddDCTError(RuntimeError):
+    """cv2.dct / cv2.idct of an odd length > 1: OpenCV raises StsNotImplemented."""
+
+
 def _dct_call(fn, block: np.ndarray) -> np.ndarray:
     x = np.ascontiguousarray(block, dtype=np.float32)
-    B = x.shape[0]
-    assert x.shape == (B, B) and B in (4, 8)
-    M = dct_matrix(B)
+    if x.ndim == 1:
+        x = x.reshape(1, -1)
+    bh, bw = x.shape
+    if not lib().oc_dct_size_ok(bh, bw):
+        raise OddDCTError("Odd-size DCT's are not implemented")
+    Mh, Mw = dct_matrix(bh), dct_matrix(bw)
     y = np.empty_like(x)
     fp = ctypes.POINTER(ctypes.c_float)
-    fn(x.ctypes.data_as(fp), B, M.ctypes.data_as(fp), y.ctypes.data_as(fp))
-    return y
+    fn(x.ctypes.data_as(fp), bh, bw, Mh.ctypes.data_as(fp), Mw.ctypes.data_as(fp), y.ctypes.data_as(fp))
+    return y.reshape(block.shape)
 
 
 def dct2d(block: np.ndarray) -> np.ndarray:
-    """cv2.dct of a float32 BxB block (orthonormal DCT-II, the oracle's fmaf chain)."""
-    return _dct_call(lib().oc_dct2d, block)
+    """cv2.dct of a float32 bh x bw block (orthonormal DCT-II rows then
+    columns, the oracle's fmaf chains); odd sides > 1 raise OddDCTError."""
+    return _dct_call(lib().oc_dct2d_rect, block)
 
 
 def idct2d(block: np.ndarray) -> np.ndarray:
-    """cv2.idct of a float32 BxB block."""
-    return _dct_call(lib().oc_idct2d, block)
+    """cv2.idct of a float32 bh x bw block."""
+    return _dct_call(lib().oc_idct2d_rect, block)
+
+
+def resize(bgr: np.ndarray, width: int, height: int) -> np.ndarray:
+    """cv2.resize(bgr, (width, height)) INTER_LINEAR 8UC3 as the oracle restates it
+    (oc_resize_bgr: copy / exact-2x area fast / fixed-point linear)."""
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    h, w = bgr.shape[:2]
+    out = np.empty((int(height), int(width), 3), np.uint8)
+    lib().oc_resize_bgr(_u8(bgr), 3 * w, w, h, _u8(out), 3 * int(width), int(width), int(height))
+    return out
+
+
+def resize_simd_end(width_bytes: int) -> int:
+    return int(lib().oc_resize_simd_end(int(width_bytes)))
 
 
 def block_quant(block: np.ndarray, q: float) -> np.ndarray:
@@ -299,11 +331,18 @@ class OracleFD:
         lib().oc_fd_prime(self._h, _u8(bgr), bgr.shape[1] * 3)
 
     def step(self, bgr: np.ndarray):
+        """(overlay, compressed, acc) of one frame (source size in, scaled size out).
+        Raises OddDCTError (with ``.overlay`` and ``.acc`` set) where the
+        reference's cv2.dct raises (fd:122)."""
         bgr = np.ascontiguousarray(bgr)
-        ov = np.empty_like(bgr)
-        cp = np.empty_like(bgr)
-        acc = np.empty(bgr.shape[:2], np.uint8)
+        ov = np.empty((self.H, self.W, 3), np.uint8)
+        cp = np.empty_like(ov)
+        acc = np.empty((self.H, self.W), np.uint8)
         rc = lib().oc_fd_step(self._h, _u8(bgr), bgr.shape[1] * 3, _u8(ov), _u8(cp), _u8(acc))
+        if rc == -6:
+            e = OddDCTError("Odd-size DCT's are not implemented")
+            e.overlay, e.acc = ov, acc
+            raise e
         if rc != 0:
             raise RuntimeError(f"oracle step failed: {rc}")
         return ov, cp, acc

@@ -313,114 +313,227 @@ void oc_dct_matrix(int B, float* M)
 }
 
 /*
- * cv2.dct -> np.round(./q)*q -> cv2.idct -> +128 -> np.clip(0,255) -> uint8
- * truncation, fd:122-125 (and of:165-168 for 8x8). Forward Y = M X M^T as a row
- * pass then a column pass, inverse X = M^T Y M likewise; each dot product is a
- * float32 fmaf chain in index order starting from the first product.
+ * cv2.dct / cv2.idct of a float32 block of bh rows x bw columns (fd:122,124;
+ * of:165-168). OpenCV transforms the rows (length bw) then the columns (length
+ * bh) — a single row or column (bh or bw = 1) is transformed as one 1-D signal
+ * and a length-1 transform is the identity — and refuses odd lengths > 1
+ * ("Odd-size DCT's are not implemented", cv::error StsNotImplemented): see
+ * oc_dct_size_ok. Here each 1-D transform is the orthonormal DCT-II matrix
+ * M_n (oc_dct_matrix; M_1 = [1]) applied as a float32 fmaf chain in index order
+ * starting from the first product — the same chains the HIP kernels run.
+ *   forward  Y = M_bh X M_bw^T : rows T[i][k] = sum_n X[i][n] M_bw[k][n],
+ *                                cols Y[k][l] = sum_i M_bh[k][i] T[i][l]
+ *   inverse  X = M_bh^T Y M_bw : rows T[k][n] = sum_l Y[k][l] M_bw[l][n],
+ *                                cols X[i][n] = sum_k M_bh[k][i] T[k][n]
  */
+int oc_dct_size_ok(int bh, int bw) { return !((bh > 1 && (bh & 1)) || (bw > 1 && (bw & 1))); }
+
+void oc_dct2d_rect(const float* X, int bh, int bw, const float* Mh, const float* Mw, float* Y)
+{
+    float* T = (float*)malloc(sizeof(float) * (size_t)bh * bw);
+    for (int i = 0; i < bh; ++i)
+        for (int k = 0; k < bw; ++k) {
+            float t = X[i * bw] * Mw[k * bw];
+            for (int n = 1; n < bw; ++n) t = fmaf(X[i * bw + n], Mw[k * bw + n], t);
+            T[i * bw + k] = t;
+        }
+    for (int k = 0; k < bh; ++k)
+        for (int l = 0; l < bw; ++l) {
+            float t = Mh[k * bh] * T[l];
+            for (int i = 1; i < bh; ++i) t = fmaf(Mh[k * bh + i], T[i * bw + l], t);
+            Y[k * bw + l] = t;
+        }
+    free(T);
+}
+
+void oc_idct2d_rect(const float* Y, int bh, int bw, const float* Mh, const float* Mw, float* X)
+{
+    float* T = (float*)malloc(sizeof(float) * (size_t)bh * bw);
+    for (int k = 0; k < bh; ++k)
+        for (int n = 0; n < bw; ++n) {
+            float t = Y[k * bw] * Mw[n];
+            for (int l = 1; l < bw; ++l) t = fmaf(Y[k * bw + l], Mw[l * bw + n], t);
+            T[k * bw + n] = t;
+        }
+    for (int i = 0; i < bh; ++i)
+        for (int n = 0; n < bw; ++n) {
+            float t = Mh[i] * T[n];
+            for (int k = 1; k < bh; ++k) t = fmaf(Mh[k * bh + i], T[k * bw + n], t);
+            X[i * bw + n] = t;
+        }
+    free(T);
+}
+
+/* Square B x B forms (kept for the golden shim and the OF path). */
+void oc_dct2d(const float* X, int B, const float* M, float* Y) { oc_dct2d_rect(X, B, B, M, M, Y); }
+void oc_idct2d(const float* Y, int B, const float* M, float* X) { oc_idct2d_rect(Y, B, B, M, M, X); }
+
+/*
+ * One static block, fd:121-125 (and of:162-168): Y - 128 -> cv2.dct ->
+ * np.round(./q)*q (float32 quotient, half-to-even) -> cv2.idct -> +128 ->
+ * np.clip(0, 255) -> truncating uint8 assignment. bh x bw block (partial blocks
+ * at the right / bottom edge are their slice, fd:121). Caller checks
+ * oc_dct_size_ok first.
+ */
+void oc_block_quant_rect(const uint8_t* in, int stride, int bh, int bw, const float* Mh, const float* Mw, float q,
+                         uint8_t* out, int ostride)
+{
+    size_t n = (size_t)bh * bw;
+    float* X = (float*)calloc(n ? n : 1, sizeof(float));
+    float* Y = (float*)calloc(n ? n : 1, sizeof(float));
+    for (int i = 0; i < bh; ++i)
+        for (int j = 0; j < bw; ++j) X[i * bw + j] = (float)in[i * stride + j] - 128.0f;
+    oc_dct2d_rect(X, bh, bw, Mh, Mw, Y);
+    for (size_t i = 0; i < n; ++i) Y[i] = rintf(Y[i] / q) * q;
+    oc_idct2d_rect(Y, bh, bw, Mh, Mw, X);
+    for (int i = 0; i < bh; ++i)
+        for (int j = 0; j < bw; ++j) {
+            float v = X[i * bw + j] + 128.0f;
+            v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+            out[i * ostride + j] = (uint8_t)v; /* truncation, as numpy's cast */
+        }
+    free(X);
+    free(Y);
+}
+
 void oc_block_quant(const uint8_t* in, int stride, int B, const float* M, float q, uint8_t* out, int ostride)
 {
-    float X[64], T[64], Y[64];
-    for (int i = 0; i < B; ++i)
-        for (int n = 0; n < B; ++n) X[i * B + n] = (float)in[i * stride + n] - 128.0f;
-    /* rows: T[i][k] = sum_n X[i][n] M[k][n] */
-    for (int i = 0; i < B; ++i)
-        for (int k = 0; k < B; ++k) {
-            float t = X[i * B] * M[k * B];
-            for (int n = 1; n < B; ++n) t = fmaf(X[i * B + n], M[k * B + n], t);
-            T[i * B + k] = t;
-        }
-    /* cols: Y[k][l] = sum_i M[k][i] T[i][l]; quantise */
-    for (int k = 0; k < B; ++k)
-        for (int l = 0; l < B; ++l) {
-            float t = M[k * B] * T[l];
-            for (int i = 1; i < B; ++i) t = fmaf(M[k * B + i], T[i * B + l], t);
-            Y[k * B + l] = rintf(t / q) * q;
-        }
-    /* inverse rows: T[k][n] = sum_l Y[k][l] M[l][n] */
-    for (int k = 0; k < B; ++k)
-        for (int n = 0; n < B; ++n) {
-            float t = Y[k * B] * M[n];
-            for (int l = 1; l < B; ++l) t = fmaf(Y[k * B + l], M[l * B + n], t);
-            T[k * B + n] = t;
-        }
-    /* inverse cols: X[i][n] = sum_k M[k][i] T[k][n] */
-    for (int i = 0; i < B; ++i)
-        for (int n = 0; n < B; ++n) {
-            float t = M[i] * T[n];
-            for (int k = 1; k < B; ++k) t = fmaf(M[k * B + i], T[k * B + n], t);
-            float v = t + 128.0f;
-            v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
-            out[i * ostride + n] = (uint8_t)v; /* truncation, as numpy's cast */
-        }
+    oc_block_quant_rect(in, stride, B, B, M, M, q, out, ostride);
 }
 
-/* The two halves of oc_block_quant as separate calls (cv2.dct / cv2.idct of a
- * float32 BxB block, same fmaf chains) — used by the golden-capture cv2 shim so
- * the reference's own numpy code performs the rounding in between. */
-void oc_dct2d(const float* X, int B, const float* M, float* Y)
+/* ------------------------------------------------------------------------- */
+/*
+ * cv2.resize(frame, (dw, dh)) of 8-bit BGR with the default INTER_LINEAR
+ * (fd:74, fd:91), restated from OpenCV 4.11 imgproc/src/resize.cpp:
+ *  - dsize == ssize: a copy;
+ *  - exact 2x downscale (scale_x == scale_y == 2.0): INTER_LINEAR becomes the
+ *    fast INTER_AREA path, (a + b + c + d + 2) >> 2 per 2x2 block and channel;
+ *  - otherwise resizeGeneric_ with fixed-point coefficients (INTER_RESIZE_COEF_
+ *    BITS = 11): per output column fx = (float)((dx + 0.5) * scale_x - 0.5),
+ *    sx = floor(fx), fx -= sx, clamped at the borders (fx = 0), alpha =
+ *    (cvRound((1 - fx) * 2048), cvRound(fx * 2048)); rows likewise. Horizontal
+ *    pass exact in int32: S = src[sx] * a0 + src[sx + 1] * a1. Vertical pass of
+ *    each output row element x (x counts bytes, 3 per pixel):
+ *      SIMD prefix (VResizeLinearVec_32s8u, 128-bit baseline: x below the end
+ *      of its 16- and 8-lane loops): ((S0 >> 4) * b0 >> 16) + ((S1 >> 4) * b1
+ *      >> 16), then (v + 2) >> 2 saturated;
+ *      scalar tail: (S0 * b0 + S1 * b1 + 2^21) >> 22 saturated.
+ * The SIMD width of the opencv-python build decides the split: parity with
+ * real OpenCV is unpinned here; the HIP kernel restates
+ * exactly this.
+ */
+static int oc_cvround_f(float v) { return (int)nearbyintf(v); }
+
+static void oc_linear_tab(int ssize, int dsize, int* ofs, int* a0, int* a1)
 {
-    float T[64];
-    for (int i = 0; i < B; ++i)
-        for (int k = 0; k < B; ++k) {
-            float t = X[i * B] * M[k * B];
-            for (int n = 1; n < B; ++n) t = fmaf(X[i * B + n], M[k * B + n], t);
-            T[i * B + k] = t;
-        }
-    for (int k = 0; k < B; ++k)
-        for (int l = 0; l < B; ++l) {
-            float t = M[k * B] * T[l];
-            for (int i = 1; i < B; ++i) t = fmaf(M[k * B + i], T[i * B + l], t);
-            Y[k * B + l] = t;
-        }
+    double inv = (double)dsize / ssize, scale = 1. / inv;
+    for (int d = 0; d < dsize; ++d) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int sx = (int)floorf(f);
+        f -= (float)sx;
+        if (sx < 0) { f = 0.f; sx = 0; }
+        if (sx >= ssize - 1) { f = 0.f; sx = ssize - 1; }
+        int c0 = oc_cvround_f((1.f - f) * 2048.f), c1 = oc_cvround_f(f * 2048.f);
+        ofs[d] = sx;
+        a0[d] = c0 < -32768 ? -32768 : (c0 > 32767 ? 32767 : c0);
+        a1[d] = c1 < -32768 ? -32768 : (c1 > 32767 ? 32767 : c1);
+    }
 }
 
-void oc_idct2d(const float* Y, int B, const float* M, float* X)
+int oc_resize_simd_end(int width)
 {
-    float T[64];
-    for (int k = 0; k < B; ++k)
-        for (int n = 0; n < B; ++n) {
-            float t = Y[k * B] * M[n];
-            for (int l = 1; l < B; ++l) t = fmaf(Y[k * B + l], M[l * B + n], t);
-            T[k * B + n] = t;
+    int x = 0;
+    while (x <= width - 16) x += 16;
+    while (x < width - 8) x += 8;
+    return x;
+}
+
+void oc_resize_bgr(const uint8_t* src, size_t spitch, int sw, int sh, uint8_t* dst, size_t dpitch, int dw, int dh)
+{
+    if (sw == dw && sh == dh) {
+        for (int y = 0; y < sh; ++y) memcpy(dst + (size_t)y * dpitch, src + (size_t)y * spitch, (size_t)3 * sw);
+        return;
+    }
+    double scx = 1. / ((double)dw / sw), scy = 1. / ((double)dh / sh);   /* cv::resize's scale_x, scale_y */
+    if (fabs(scx - 2.0) < 2.220446049250313e-16 && fabs(scy - 2.0) < 2.220446049250313e-16) {
+        for (int y = 0; y < dh; ++y)
+            for (int x = 0; x < 3 * dw; ++x) {
+                int c = x % 3, sx = 2 * (x / 3);
+                const uint8_t* r0 = src + (size_t)(2 * y) * spitch;
+                const uint8_t* r1 = r0 + spitch;
+                int s = r0[3 * sx + c] + r0[3 * sx + 3 + c] + r1[3 * sx + c] + r1[3 * sx + 3 + c];
+                dst[(size_t)y * dpitch + x] = (uint8_t)((s + 2) >> 2);
+            }
+        return;
+    }
+    int *xo = (int*)malloc(sizeof(int) * dw * 3), *xa = xo + dw, *xb = xa + dw;
+    int *yo = (int*)malloc(sizeof(int) * dh * 3), *ya = yo + dh, *yb = ya + dh;
+    oc_linear_tab(sw, dw, xo, xa, xb);
+    oc_linear_tab(sh, dh, yo, ya, yb);
+    int wb = 3 * dw, xs = oc_resize_simd_end(wb);
+    for (int y = 0; y < dh; ++y) {
+        const uint8_t* r0 = src + (size_t)yo[y] * spitch;
+        const uint8_t* r1 = src + (size_t)(yo[y] + 1 < sh ? yo[y] + 1 : sh - 1) * spitch;
+        int b0 = ya[y], b1 = yb[y];
+        for (int x = 0; x < wb; ++x) {
+            int d = x / 3, c = x % 3, sx = xo[d], sx1 = sx + 1 < sw ? sx + 1 : sx;
+            int S0 = r0[3 * sx + c] * xa[d] + r0[3 * sx1 + c] * xb[d];
+            int S1 = r1[3 * sx + c] * xa[d] + r1[3 * sx1 + c] * xb[d];
+            int v;
+            if (x < xs) {
+                int h0 = ((S0 >> 4) * b0) >> 16, h1 = ((S1 >> 4) * b1) >> 16;
+                v = (h0 + h1 + 2) >> 2;
+            } else {
+                v = (int)(((int64_t)S0 * b0 + (int64_t)S1 * b1 + (1 << 21)) >> 22);
+            }
+            dst[(size_t)y * dpitch + x] = sat_u8i(v);
         }
-    for (int i = 0; i < B; ++i)
-        for (int n = 0; n < B; ++n) {
-            float t = M[i] * T[n];
-            for (int k = 1; k < B; ++k) t = fmaf(M[k * B + i], T[k * B + n], t);
-            X[i * B + n] = t;
-        }
+    }
+    free(xo);
+    free(yo);
 }
 
 /* ------------------------------------------------------------------------- */
 /* The per-feed worker (fd:67-133).                                           */
 struct oc_fd {
     dvc_fd_params p;
-    int primed;
+    int primed, failed;
+    int sw, sh;                 /* source frame size (resized to p.width x p.height, fd:74,91) */
     uint16_t k5[5];
     uint16_t kp[64];
-    float M[64];
-    uint8_t *prev, *gray, *cur, *motion, *filtered, *filled, *dil, *acc, *ycc;
+    float *Mb, *Mw, *Mh;        /* DCT bases of length B, W % B, H % B */
+    uint8_t *prev, *gray, *cur, *motion, *filtered, *filled, *dil, *acc, *ycc, *scaled, *Yb, *Yq;
     dvc_fd_stats st;
     int use_literal;
 };
 
 oc_fd* oc_fd_create(const dvc_fd_params* p, int use_literal)
 {
-    if (p->width < 1 || p->height < 1 || p->block < 1 || p->block > 8 || p->ksize < 1 || p->ksize > 63)
+    if (p->width < 1 || p->height < 1 || p->block < 1 || p->block > 1024 || p->ksize < 1 || p->ksize > 63)
         return NULL;
+    if (p->src_width < 0 || p->src_height < 0) return NULL;
     oc_fd* h = (oc_fd*)calloc(1, sizeof(oc_fd));
     h->p = *p;
     h->use_literal = use_literal;
+    h->sw = p->src_width ? p->src_width : p->width;
+    h->sh = p->src_height ? p->src_height : p->height;
     oc_gauss_kernel_q8(5, 0.0, h->k5);
     if (oc_gauss_kernel_q8(p->prime_ksize, p->prime_sigma, h->kp) != 0) { free(h); return NULL; }
-    oc_dct_matrix(p->block, h->M);
+    int B = p->block, bw = p->width % B, bh = p->height % B;
+    h->Mb = (float*)malloc(sizeof(float) * B * B);
+    h->Mw = (float*)malloc(sizeof(float) * (bw ? bw * bw : 1));
+    h->Mh = (float*)malloc(sizeof(float) * (bh ? bh * bh : 1));
+    oc_dct_matrix(B, h->Mb);
+    if (bw) oc_dct_matrix(bw, h->Mw);
+    if (bh) oc_dct_matrix(bh, h->Mh);
     size_t N = (size_t)p->width * p->height;
     h->prev = (uint8_t*)calloc(N, 1); h->gray = (uint8_t*)calloc(N, 1);
     h->cur = (uint8_t*)calloc(N, 1); h->motion = (uint8_t*)calloc(N, 1);
     h->filtered = (uint8_t*)calloc(N, 1); h->filled = (uint8_t*)calloc(N, 1);
     h->dil = (uint8_t*)calloc(N, 1); h->acc = (uint8_t*)calloc(N, 1);
     h->ycc = (uint8_t*)calloc(N * 3, 1);
+    h->scaled = (uint8_t*)calloc(N * 3, 1);
+    h->Yb = (uint8_t*)calloc((size_t)B * B, 1); h->Yq = (uint8_t*)calloc((size_t)B * B, 1);
     return h;
 }
 
@@ -428,29 +541,47 @@ void oc_fd_destroy(oc_fd* h)
 {
     if (!h) return;
     free(h->prev); free(h->gray); free(h->cur); free(h->motion); free(h->filtered);
-    free(h->filled); free(h->dil); free(h->acc); free(h->ycc); free(h);
+    free(h->filled); free(h->dil); free(h->acc); free(h->ycc); free(h->scaled);
+    free(h->Yb); free(h->Yq); free(h->Mb); free(h->Mw); free(h->Mh); free(h);
+}
+
+/* cv2.resize(frame, (scaled_width, scaled_height)) (fd:74, fd:91): the frame
+ * itself when the sizes agree, else the resized copy. */
+static const uint8_t* oc_fd_input(oc_fd* h, const uint8_t* bgr, size_t* pitch)
+{
+    int W = h->p.width, H = h->p.height;
+    if (h->sw == W && h->sh == H) return bgr;
+    oc_resize_bgr(bgr, *pitch, h->sw, h->sh, h->scaled, (size_t)3 * W, W, H);
+    *pitch = (size_t)3 * W;
+    return h->scaled;
 }
 
 /* fd:67-81 */
 int oc_fd_prime(oc_fd* h, const uint8_t* bgr, size_t pitch)
 {
     int W = h->p.width, H = h->p.height;
-    oc_bgr2gray(bgr, pitch, W, H, h->gray);
-    oc_gaussian_q8(h->gray, W, H, h->kp, h->p.prime_ksize, h->prev);
-    memset(h->acc, 0, (size_t)W * H);
+    bgr = oc_fd_input(h, bgr, &pitch);                                      /* fd:74 */
+    oc_bgr2gray(bgr, pitch, W, H, h->gray);                                 /* fd:75 */
+    oc_gaussian_q8(h->gray, W, H, h->kp, h->p.prime_ksize, h->prev);        /* fd:77 */
+    memset(h->acc, 0, (size_t)W * H);                                       /* fd:81 */
     memset(&h->st, 0, sizeof(h->st));
     h->primed = 1;
+    h->failed = 0;
     return 0;
 }
 
-/* fd:91-133 */
+/* fd:91-133. Returns DVC_E_ODD_DCT when a static block has an odd side > 1
+ * (cv2.dct raises, fd:122; the reference's try/except ends the loop, fd:140):
+ * the overlay of that frame is written (fd:112 precedes the block loop), the
+ * compressed frame is not, the frame is not counted and the worker stops. */
 int oc_fd_step(oc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay,
                uint8_t* compressed, uint8_t* acc_out)
 {
-    if (!h->primed) return DVC_E_STATE;
+    if (!h->primed || h->failed) return DVC_E_STATE;
     const dvc_fd_params* p = &h->p;
     int W = p->width, H = p->height, B = p->block;
     size_t N = (size_t)W * H;
+    bgr = oc_fd_input(h, bgr, &pitch);                                     /* fd:91 */
     oc_bgr2gray(bgr, pitch, W, H, h->gray);                               /* fd:92 */
     oc_gaussian_q8(h->gray, W, H, h->k5, 5, h->cur);                       /* fd:93 */
     oc_absdiff_threshold(h->prev, h->cur, N, p->ithresh, h->motion);       /* fd:96-97 */
@@ -474,9 +605,10 @@ int oc_fd_step(oc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay,
             oc_bgr2ycrcb_px(s + 3 * x, h->ycc + 3 * i);
         }
     }
-    /* fd:117-127: blocks (partial blocks at the edge included) */
+    if (acc_out) memcpy(acc_out, h->acc, N);
+    /* fd:117-127: B x B blocks in row-major order; the right / bottom edge blocks
+     * are their partial slices (fd:120-121) */
     uint64_t nstatic = 0;
-    uint8_t Yb[64], Yq[64];
     for (int by = 0; by < H; by += B)
         for (int bx = 0; bx < W; bx += B) {
             int bh = by + B <= H ? B : H - by, bw = bx + B <= W ? B : W - bx;
@@ -484,21 +616,21 @@ int oc_fd_step(oc_fd* h, const uint8_t* bgr, size_t pitch, uint8_t* overlay,
             for (int i = 0; i < bh && zero; ++i)
                 for (int j = 0; j < bw; ++j)
                     if (h->acc[(size_t)(by + i) * W + bx + j]) { zero = 0; break; }
-            if (!zero) continue;
-            if (bh != B || bw != B) return DVC_E_UNSUPPORTED; /* partial DCT: GPU path rejects too */
+            if (!zero) continue;                                           /* fd:120 mean() == 0 */
+            if (!oc_dct_size_ok(bh, bw)) { h->failed = 1; return DVC_E_ODD_DCT; }
             ++nstatic;
-            for (int i = 0; i < B; ++i)
-                for (int j = 0; j < B; ++j) Yb[i * B + j] = h->ycc[3 * ((size_t)(by + i) * W + bx + j)];
-            oc_block_quant(Yb, B, B, h->M, p->quant, Yq, B);
-            for (int i = 0; i < B; ++i)
-                for (int j = 0; j < B; ++j) {
+            for (int i = 0; i < bh; ++i)
+                for (int j = 0; j < bw; ++j) h->Yb[i * bw + j] = h->ycc[3 * ((size_t)(by + i) * W + bx + j)];
+            oc_block_quant_rect(h->Yb, bw, bh, bw, bh == B ? h->Mb : h->Mh, bw == B ? h->Mb : h->Mw, p->quant,
+                                h->Yq, bw);
+            for (int i = 0; i < bh; ++i)
+                for (int j = 0; j < bw; ++j) {
                     uint8_t* c = h->ycc + 3 * ((size_t)(by + i) * W + bx + j);
-                    c[0] = Yq[i * B + j]; c[1] = 128; c[2] = 128;
+                    c[0] = h->Yq[i * bw + j]; c[1] = 128; c[2] = 128;      /* fd:125-127 */
                 }
         }
     if (compressed)                                                         /* fd:129-130 */
         for (size_t i = 0; i < N; ++i) oc_ycrcb2bgr_px(h->ycc + 3 * i, compressed + 3 * i);
-    if (acc_out) memcpy(acc_out, h->acc, N);
     uint8_t* t = h->prev; h->prev = h->cur; h->cur = t;                    /* fd:133 */
     uint64_t nm = 0;
     for (size_t i = 0; i < N; ++i) nm += h->motion[i] != 0;
@@ -533,4 +665,5 @@ void oc_fd_set_state(oc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
     memcpy(h->prev, prev_gray, N);
     memcpy(h->acc, acc, N);
     h->primed = 1;
+    h->failed = 0;
 }

@@ -25,6 +25,13 @@ void oc_dct_matrix(int B, float* M);
 void oc_dct2d(const float* X, int B, const float* M, float* Y);
 void oc_idct2d(const float* Y, int B, const float* M, float* X);
 void oc_block_quant(const uint8_t* in, int stride, int B, const float* M, float q, uint8_t* out, int ostride);
+int oc_dct_size_ok(int bh, int bw);
+void oc_dct2d_rect(const float* X, int bh, int bw, const float* Mh, const float* Mw, float* Y);
+void oc_idct2d_rect(const float* Y, int bh, int bw, const float* Mh, const float* Mw, float* X);
+void oc_block_quant_rect(const uint8_t* in, int stride, int bh, int bw, const float* Mh, const float* Mw, float q,
+                         uint8_t* out, int ostride);
+int oc_resize_simd_end(int width);
+void oc_resize_bgr(const uint8_t* src, size_t spitch, int sw, int sh, uint8_t* dst, size_t dpitch, int dw, int dh);
 
 typedef struct oc_fd oc_fd;
 oc_fd* oc_fd_create(const dvc_fd_params* p, int use_literal);

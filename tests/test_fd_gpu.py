@@ -12,15 +12,32 @@ pytestmark = pytest.mark.gpu
 PLANES = {"gray": 0, "motion": 1, "filtered": 2, "acc": 3, "dilated": 4}
 
 
-def _run_pair(dvc_amd, oracle, frames, **kw):
-    H, W = frames.shape[1:3]
+def _run_pair(dvc_amd, oracle, frames, scale=None, **kw):
+    """Per-frame GPU vs oracle on every plane, output and counter. ``scale``:
+    (W, H) of the scaled frames (the frames given are the source size)."""
+    SH, SW = frames.shape[1:3]
+    W, H = scale or (SW, SH)
+    if scale:
+        kw = dict(kw, src_width=SW, src_height=SH)
     gpu = dvc_amd.FDWorker(W, H, device=0, keep_planes=True, **kw)
     ref = oracle.OracleFD(W, H, **kw)
     gpu.prime(frames[0])
     ref.prime(frames[0])
     for t in range(1, len(frames)):
+        try:
+            rov, rcp, racc = ref.step(frames[t])
+        except oracle.OddDCTError as e:          # the reference stops here (fd:122, fd:140)
+            from dvc_amd._native import DVC_E_ODD_DCT, DvcError
+            ov = np.empty((H, W, 3), np.uint8)
+            with pytest.raises(DvcError) as ei:
+                gpu.step(frames[t], ov)
+            assert ei.value.code == DVC_E_ODD_DCT
+            assert np.array_equal(ov, e.overlay), f"overlay of the stopping frame {t} differs"
+            assert gpu.stats()["frames"] == ref.stats()["frames"] == t - 1
+            gpu.close()
+            ref.close()
+            return None
         ov, cp = gpu.step(frames[t])
-        rov, rcp, racc = ref.step(frames[t])
         for name, idx in PLANES.items():
             g, r = gpu.plane(idx), ref.plane(idx)
             if not np.array_equal(g, r):
@@ -228,9 +245,9 @@ def test_batch_device_matches_steps(gpu_lib):
 def test_errors(gpu_lib):
     from dvc_amd._native import DvcError
     with pytest.raises(DvcError):
-        gpu_lib.FDWorker(642, 360)            # not a multiple of the block
+        gpu_lib.FDWorker(640, 360, block_size=65)   # the GPU path implements block sizes 1..64
     with pytest.raises(DvcError):
-        gpu_lib.FDWorker(640, 360, block_size=16)
+        gpu_lib.FDWorker(8, 360)                    # frames of at least 16 x 16
     w = gpu_lib.FDWorker(640, 360)
     with pytest.raises(DvcError):
         w.step(np.zeros((360, 640, 3), np.uint8))   # step before prime
@@ -249,3 +266,113 @@ def test_process_single_video_fd(gpu_lib, tmp_path):
     txt = (d / "execution_times.txt").read_text().splitlines()
     assert txt[0] == "Frame Differencing:" and txt[1] == "  Frames processed: 101"
     assert (d / "processing.log").exists()
+
+
+# ---------------------------------------------------------------- geometry ---
+# Any frame size and block size (fd:117-127: partial edge blocks are their
+# slices; an odd side > 1 of a static block stops the reference, fd:122/140),
+# and scale_factor (fd:60-61, 74, 91: the GPU resizes).
+@pytest.mark.parametrize("W,H,n,kw", [
+    (960, 540, 12, dict(block_size=8, kernel_size=10, release_factor=0.3)),   # __main__ kwargs at 1080p / 2
+    (1366, 768, 11, {}),                        # W % 4 = 2: re-pitched rows, 2-px edge blocks
+    (641, 361, 11, {}),                         # 1-px edge blocks (length-1 DCTs)
+    (643, 360, 12, {}),                         # 3-px edge blocks: stops at the first static one
+    (162, 98, 11, dict(block_size=2, min_area=20)),
+    (200, 120, 11, dict(block_size=16)),
+    (200, 122, 11, dict(block_size=6, kernel_size=4)),
+    (130, 70, 11, dict(block_size=1, min_area=10)),
+    (258, 194, 11, dict(block_size=64)),
+    (300, 200, 11, dict(block_size=5)),         # odd block: stops once a block is static
+])
+def test_fd_parity_geometry(gpu_lib, oracle_lib, W, H, n, kw):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=W + H, n_objects=4), **kw)
+
+
+@pytest.mark.parametrize("SW,SH,W,H,kw", [
+    (1920, 1080, 960, 540, dict(block_size=8, kernel_size=10, release_factor=0.3)),   # fd:200-207
+    (640, 360, 448, 252, {}),                   # scale 0.7: INTER_LINEAR fixed point
+    (320, 180, 416, 234, dict(block_size=6)),   # scale 1.3: upscale
+    (641, 361, 320, 180, {}),                   # about 0.5 of odd sizes: linear, not the 2x area path
+])
+def test_fd_parity_scaled(gpu_lib, oracle_lib, SW, SH, W, H, kw):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(SW, SH, 9, seed=SW, n_objects=4), scale=(W, H), **kw)
+
+
+@pytest.mark.parametrize("W,H,batch,kw", [
+    (1366, 768, 5, {}),
+    (962, 542, 4, dict(block_size=8)),
+    (200, 122, 3, dict(block_size=6)),
+])
+def test_geometry_batch_device_matches_oracle(gpu_lib, oracle_lib, W, H, batch, kw):
+    """Dense (n, H, W, 3) device frames of any width (rows not 4-byte aligned ->
+    re-pitched on the device), batched, vs the oracle frame by frame."""
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, 10, seed=3, n_objects=5)
+    rov, rcp, rplanes, rst = _oracle_sequence(oracle_lib, frames, **kw)
+    d = torch.from_numpy(frames).to("cuda:0")
+    ov = torch.empty_like(d[1:])
+    cp = torch.empty_like(d[1:])
+    w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=batch, **kw)
+    w.prime(d[0])
+    w.step_batch(d[1:], ov, cp)
+    w.sync()
+    assert np.array_equal(ov.cpu().numpy(), rov) and np.array_equal(cp.cpu().numpy(), rcp)
+    assert w.stats() == rst
+    w.close()
+
+
+def test_odd_stop_in_batch(gpu_lib, oracle_lib):
+    """A batch crossing the stopping frame: frames before it complete, its
+    overlay valid, stats count the completed frames (host and device mode)."""
+    import torch
+    from dvc_amd._native import DVC_E_ODD_DCT, DvcError
+    from dvc_amd.synthetic import clip
+    W, H = 643, 360
+    frames = clip(W, H, 14, seed=9)
+    ref = oracle_lib.OracleFD(W, H)
+    ref.prime(frames[0])
+    rov = []
+    for f in frames[1:]:
+        try:
+            rov.append(ref.step(f)[0])
+        except oracle_lib.OddDCTError as e:
+            rov.append(e.overlay)
+            break
+    k = ref.stats()["frames"]
+    assert 0 < k < len(frames) - 2
+    w = gpu_lib.FDWorker(W, H, max_batch=4)
+    w.prime(frames[0])
+    ov = np.empty((13, H, W, 3), np.uint8)
+    with pytest.raises(DvcError) as ei:
+        w.step_batch(frames[1:], ov, np.empty_like(ov))
+    assert ei.value.code == DVC_E_ODD_DCT and w.stats()["frames"] == k
+    assert all(np.array_equal(ov[t], rov[t]) for t in range(k + 1))
+    with pytest.raises(DvcError):
+        w.step(frames[1])                       # stopped until the next prime
+    w.prime(frames[0])
+    w.step(frames[1])
+    w.close()
+    d = torch.from_numpy(frames).to("cuda:0")
+    wd = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=5)
+    wd.prime(d[0])
+    dov = torch.empty_like(d[1:])
+    wd.step_batch(d[1:], dov, torch.empty_like(dov))   # asynchronous: reported at the sync
+    with pytest.raises(DvcError) as ei:
+        wd.sync()
+    assert ei.value.code == DVC_E_ODD_DCT and wd.stats()["frames"] == k
+    assert all(np.array_equal(dov[t].cpu().numpy(), rov[t]) for t in range(k + 1))
+    wd.close()
+
+
+def test_contour_filter_any_width(gpu_lib, oracle_lib):
+    rng = np.random.default_rng(77)
+    for _ in range(40):
+        H, W = int(rng.integers(4, 90)), int(rng.integers(4, 300))
+        m = (rng.random((H, W)) < rng.uniform(0.05, 0.9)).astype(np.uint8) * 255
+        ma2 = int(rng.integers(-1, 40))
+        g, gn = gpu_lib._native.contour_filter(m, ma2)
+        r, rn, _ = oracle_lib.contour_filter(m, ma2)
+        assert gn == rn and np.array_equal(g, r), (H, W, ma2)

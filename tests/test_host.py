@@ -99,15 +99,63 @@ def test_synthetic_deterministic_and_moving():
     assert 0 < (d != 0).any(-1).mean() < 0.01 and np.abs(d).max() <= 3
 
 
-def test_resize_frame_semantics():
-    from dvc_amd.frame_differencing import resize_frame
-    f = np.random.default_rng(1).integers(0, 256, (8, 10, 3), dtype=np.uint8)
-    assert resize_frame(f, (10, 8)) is f
-    h = resize_frame(f, (5, 4))
-    exp = (f[0::2, 0::2].astype(int) + f[0::2, 1::2] + f[1::2, 0::2] + f[1::2, 1::2] + 2) >> 2
-    assert np.array_equal(h, exp)
-    with pytest.raises(NotImplementedError):
-        resize_frame(f, (7, 5))
+def _np_linear_tab(ssize, dsize):
+    """Independent numpy restatement of resizeGeneric_'s INTER_LINEAR tables."""
+    scale = 1.0 / (dsize / ssize)
+    d = np.arange(dsize)
+    f = ((d + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    lo, hi = s < 0, s >= ssize - 1
+    f[lo | hi] = 0
+    s[lo] = 0
+    s[hi] = ssize - 1
+    a0 = np.rint((np.float32(1) - f) * np.float32(2048)).astype(np.int64)
+    a1 = np.rint(f * np.float32(2048)).astype(np.int64)
+    return s, a0, a1
+
+
+def _np_resize(img, dw, dh):
+    sh, sw = img.shape[:2]
+    if (sw, sh) == (dw, dh):
+        return img.copy()
+    if sw == 2 * dw and sh == 2 * dh:
+        f = img.astype(np.int64)
+        return ((f[0::2, 0::2] + f[0::2, 1::2] + f[1::2, 0::2] + f[1::2, 1::2] + 2) >> 2).astype(np.uint8)
+    xs, xa, xb = _np_linear_tab(sw, dw)
+    ys, ya, yb = _np_linear_tab(sh, dh)
+    src = img.astype(np.int64)
+    xs1 = np.minimum(xs + 1, sw - 1)
+    Hrow = src[:, xs] * xa[None, :, None] + src[:, xs1] * xb[None, :, None]       # sh x dw x 3
+    S0, S1 = Hrow[ys].reshape(dh, -1), Hrow[np.minimum(ys + 1, sh - 1)].reshape(dh, -1)
+    b0, b1 = ya[:, None], yb[:, None]
+    simd = ((((S0 >> 4) * b0) >> 16) + (((S1 >> 4) * b1) >> 16) + 2) >> 2
+    scal = (S0 * b0 + S1 * b1 + (1 << 21)) >> 22
+    w = 3 * dw
+    x = 0
+    while x <= w - 16:
+        x += 16
+    while x < w - 8:
+        x += 8
+    out = np.where(np.arange(w)[None, :] < x, simd, scal)
+    return np.clip(out, 0, 255).astype(np.uint8).reshape(dh, dw, 3)
+
+
+@pytest.mark.parametrize("sw,sh,dw,dh", [(10, 8, 10, 8), (10, 8, 5, 4), (200, 120, 140, 84), (120, 80, 156, 104),
+                                         (64, 48, 37, 29), (33, 17, 66, 34), (1920, 1080, 960, 540),
+                                         (1366, 768, 683, 384), (1365, 767, 682, 383)])
+def test_oracle_resize_matches_numpy_restatement(oracle_lib, sw, sh, dw, dh):
+    """cv2.resize INTER_LINEAR 8UC3 (fd:74,91): the C oracle vs an independent
+    numpy restatement (copy / exact-2x area fast / fixed-point linear with the
+    128-bit SIMD rounding prefix). OpenCV itself is absent: parity unpinned."""
+    img = np.random.default_rng(sw * 7 + dh).integers(0, 256, (sh, sw, 3), dtype=np.uint8)
+    assert np.array_equal(oracle_lib.resize(img, dw, dh), _np_resize(img, dw, dh))
+
+
+def test_resize_simd_split():
+    import oracle
+    assert [oracle.resize_simd_end(w) for w in (3, 8, 9, 15, 16, 17, 24, 25, 2880, 360)] == \
+        [0, 0, 8, 8, 16, 16, 16, 24, 2880, 352]
 
 
 def test_video_name():
