@@ -40,6 +40,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -77,11 +78,13 @@ def pmc_traffic(path: str, kernel_prefix: str, workload: str, frames_per_launch:
         return None
 
 
-def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path: str = "fd"):
+def _cpu_feed(job):
+    """One feed through the C oracle on this process's core: (frames, seconds)."""
+    width, height, budget_s, max_frames, path, seed = job
+    sys.path.insert(0, ROOT)
     import oracle  # checker / CPU baseline only
     from dvc_amd.synthetic import SyntheticClip
-    oracle.build()
-    clip = SyntheticClip(width, height, seed=0)
+    clip = SyntheticClip(width, height, seed=seed)
     o = oracle.OracleFD(width, height) if path == "fd" else oracle.OracleOF(width, height)
     o.prime(clip.frame(0))
     frames = [clip.frame(t) for t in range(1, max_frames + 1)]
@@ -93,9 +96,34 @@ def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path
             break
     dt = time.perf_counter() - t0
     o.close()
-    return {"value": round(n * width * height / dt / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": f"C oracle (oracle/{'dvc' if path == 'fd' else 'of'}_oracle.c, -O3, 1 thread) on frames 1..{n} of the same "
-                      f"{width}x{height} synthetic feed (seed 0), {dt:.1f} s"}
+    return n, dt
+
+
+def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path: str = "fd", cores: int = 1):
+    """The C oracle on the host: `cores` independent feeds (seeds 0..cores-1) on
+    as many processes, each a bounded sample of ~budget_s; value = the sum of
+    their Mpx/s (the CPU analogue of feed-per-GPU)."""
+    import oracle  # checker / CPU baseline only
+    oracle.build()
+    jobs = [(width, height, budget_s, max_frames, path, c) for c in range(max(1, cores))]
+    if len(jobs) == 1:
+        res = [_cpu_feed(jobs[0])]
+    else:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(len(jobs)) as pool:   # fresh interpreters: no GPU state inherited
+            res = pool.map(_cpu_feed, jobs)
+    value = sum(n * width * height / dt for n, dt in res) / 1e6
+    nf = sum(n for n, _ in res)
+    secs = max(dt for _, dt in res)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count()
+    src = f"oracle/{'dvc' if path == 'fd' else 'of'}_oracle.c"
+    return {"value": round(value, 3), "unit": "Mpixels/s", "cores": len(jobs), "kind": "port",
+            "nproc": os.cpu_count(), "cpus_available": avail,
+            "sample": f"C oracle ({src}, -O3, 1 thread per feed) on {len(jobs)} feed(s) of the same {width}x{height} "
+                      f"synthetic workload (seeds 0..{len(jobs) - 1}), {nf} frames in {secs:.1f} s"}
 
 
 def main():
@@ -117,6 +145,14 @@ def main():
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per device launch (max_batch; 0: fd 383 at 1080p, scaled by pixels / of 16)")
     ap.add_argument("--per-frame", action="store_true", help="one dvc_fd_step per frame instead of batches")
+    ap.add_argument("--io", choices=("device", "host-pinned", "host-pageable"), default="device",
+                    help="device: frames and outputs resident in HBM (the headline); host-*: frames from and "
+                         "outputs to host memory through the C-ABI's host-pointer path (PCIe-inclusive; pinned = "
+                         "dvc_host_alloc buffers DMA'd directly, pageable = numpy arrays staged by the library)")
+    ap.add_argument("--feeds", type=int, default=1,
+                    help="independent feeds per GPU, one handle and one host thread each (config 4's unit)")
+    ap.add_argument("--cpu-cores", type=int, default=1,
+                    help="CPU baseline: this many feeds on this many host processes (1 = single core)")
     args = ap.parse_args()
 
     import numpy as np
@@ -135,37 +171,52 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     W, H = args.width, args.height
-    # FD: 383-frame launches at 1080p (scaled by pixel count for larger frames)
+    of = args.path == "of"
+    host_io = args.io != "device"
+    # FD: 383-frame launches at 1080p (scaled by pixel count for larger frames);
+    # host I/O: 32-frame chunks (the library pipelines chunk uploads / downloads)
     fd_batch = max(31, min(383, 383 * 1920 * 1080 // (W * H)))
-    R = args.ring or (64 if args.path == "of" else fd_batch + 1)
-    clip = SyntheticClip(W, H, seed=rank, noisy=args.noisy)
+    R = args.ring or (64 if (of or host_io) else fd_batch + 1)
     order = pingpong(R)
     P = len(order)                 # frames per step (126 for R=64)
-    # frame j of a step is ring frame order[(j + 1) % P] (frame 0 primes the feed)
-    seq = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
-    for i in range(R):
-        f = torch.from_numpy(clip.frame(i)).to(dev)
-        for j in range(P):
-            if order[(j + 1) % P] == i:
-                seq[j].copy_(f)
-    first = torch.from_numpy(clip.frame(0)).to(dev)
-    ov = torch.empty_like(seq)
-    cp = torch.empty_like(seq)
-    torch.cuda.synchronize()
-    of = args.path == "of"
-    if of:   # the OF worker writes a mask plane instead of the red overlay
-        ov = torch.empty((P, H, W), dtype=torch.uint8, device=dev)
-    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else fd_batch), P))
+    batch = 1 if args.per_frame else max(1, min(args.batch or (16 if of else (32 if host_io else fd_batch)), P))
+    F = max(1, args.feeds)
 
-    def make_worker(ktiming=False):
+    # per feed: its own synthetic camera (seed = global feed index); frame j of
+    # a step is ring frame order[(j + 1) % P] (frame 0 primes the feed)
+    def feed_inputs(f):
+        clip = SyntheticClip(W, H, seed=rank * F + f, noisy=args.noisy)
+        ring = [clip.frame(i) for i in range(R)]
+        idx = [order[(j + 1) % P] for j in range(P)]
+        oshape = (P, H, W) if of else (P, H, W, 3)     # OF writes a mask plane instead of the red overlay
+        if args.io == "device":
+            seq = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
+            for j in range(P):
+                seq[j].copy_(torch.from_numpy(ring[idx[j]]))
+            outs = (torch.empty(oshape, dtype=torch.uint8, device=dev),
+                    torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev))
+        else:
+            alloc = dvc_amd._native.pinned if args.io == "host-pinned" else (lambda shp: np.empty(shp, np.uint8))
+            seq = alloc((P, H, W, 3))
+            for j in range(P):
+                seq[j] = ring[idx[j]]
+            outs = (alloc(oshape), alloc((P, H, W, 3)))
+        first = torch.from_numpy(ring[0]).to(dev) if args.io == "device" else ring[0]
+        return seq, outs, first
+
+    inputs = [feed_inputs(f) for f in range(F)]
+    torch.cuda.synchronize()
+
+    def make_worker(f, ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
         kw = {} if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
                                 release_factor=args.release_factor)
-        w = cls(W, H, device=local, device_ptrs=True, ktiming=ktiming, max_batch=batch, **kw)
-        w.prime(first)
+        w = cls(W, H, device=local, device_ptrs=not host_io, ktiming=ktiming, max_batch=batch, **kw)
+        w.prime(inputs[f][2])
         return w
 
-    def run_steps(w, n):
+    def run_feed(w, f, n):
+        seq, (ov, cp), _ = inputs[f]
         for _ in range(n):
             if args.per_frame:
                 for j in range(P):
@@ -173,9 +224,29 @@ def main():
             else:
                 w.step_batch(seq, ov, cp)
 
-    w = make_worker()
-    run_steps(w, args.warmup)
-    w.sync()
+    def run_steps(ws, n):
+        if len(ws) == 1:
+            run_feed(ws[0], 0, n)
+        else:   # one host thread per feed (ctypes releases the GIL)
+            errs = []
+
+            def go(f):
+                try:
+                    run_feed(ws[f], f, n)
+                except Exception as e:  # re-raised below
+                    errs.append(e)
+            ths = [threading.Thread(target=go, args=(f,)) for f in range(len(ws))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            if errs:
+                raise errs[0]
+        for w in ws:
+            w.sync()
+
+    ws = [make_worker(f) for f in range(F)]
+    run_steps(ws, args.warmup)
 
     def barrier():
         if world > 1:
@@ -184,21 +255,23 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    run_steps(w, args.steps)
-    w.sync()
+    run_steps(ws, args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    st = w.stats()
-    w.close()
+    sts = [w.stats() for w in ws]
+    st = {k: sum(x[k] for x in sts) for k in sts[0]}
+    for w in ws:
+        w.close()
 
-    # dominant kernel: hipEvent-timed k_out launches (on the back stream), same steps
-    wk = make_worker(ktiming=True)
-    run_steps(wk, 1)
+    # dominant kernel: hipEvent-timed launches (k_out on the back stream / k_flow
+    # level 0 on the flow stream) of feed 0 alone, same steps
+    wk = make_worker(0, ktiming=True)
+    run_steps([wk], 1)
     wk.ktime(reset=True)
     ksteps = max(1, min(args.steps, 10))
-    run_steps(wk, ksteps)
+    run_steps([wk], ksteps)
     kms, kn = wk.ktime()
     wk.close()
     kframes = ksteps * P
@@ -211,13 +284,17 @@ def main():
         dist.all_reduce(vec, op=dist.ReduceOp.SUM)   # RCCL: end-of-run aggregate stats only
         vec[0] = tmax[0]
     elapsed_max = float(vec[0])
-    frames_total = args.steps * P * world
+    frames_total = args.steps * P * F * world
     value = frames_total * W * H / elapsed_max / 1e6
 
     if rank == 0:
         avg_ms = kms / max(kn, 1)
         res = f"{W}x{H}" if (W, H) != (1920, 1080) else "1080p"
-        workload = f"{args.path}_{res}_single_feed_per_gpu"
+        workload = f"{args.path}_{res}_single_feed_per_gpu" if F == 1 else f"{args.path}_{res}_{F}_feeds_per_gpu"
+        if host_io:
+            workload += f"_{args.io}_io"
+        if args.per_frame:
+            workload += "_per_frame"
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
             workload += f"_b{args.block_size}_k{args.kernel_size}_r{args.release_factor:g}"
         if of:   # kn counts level-0 k_flow launches (iterations per batch)
@@ -249,23 +326,25 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload, "path": "optical-flow (motion_compression_opt.py)" if of
                        else "frame-differencing (frame_differencing.py)",
-                       "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": 1,
+                       "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": F,
+                       "io": args.io + (" (PCIe-inclusive: frames up, both outputs down)" if host_io else ""),
                        "ring_frames": R, "noisy": args.noisy,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
-                       "fps_per_gpu": round(args.steps * P / elapsed_max, 1),
+                       "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),
                        "pipeline_bytes_per_px": pipe,
-                       "pipeline_GBps_per_gpu": round(pipe * args.steps * P * W * H / elapsed_max / 1e9, 1)},
+                       "pipeline_GBps_per_gpu": round(pipe * args.steps * P * F * W * H / elapsed_max / 1e9, 1)},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch),
                          "frames_per_launch": round(per_launch_frames, 2),
-                         "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn},
+                         "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn,
+                         "timed_with": "feed 0 alone"},
             "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
                       "static_blocks": int(vec[4])},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path)
+            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path, args.cpu_cores)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
