@@ -386,11 +386,16 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     // call, and work queued on it after the call waits for the call's outputs.
     int plo = 0, phi = 0;
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
-    auto mk = [](hipStream_t* st, int prio) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio); };
-    if ((e = mk(&h->stream, phi)) != hipSuccess) return bad(e, "hipStreamCreate");
+    // priorities of the front, contour-filter, accumulate and output streams:
+    // 'l'ow, 'n'ormal, 'h'igh; DVC_PRIO overrides for sweeps (default "lhhn")
+    static const char* prio = [] { const char* e = getenv("DVC_PRIO"); return e && strlen(e) == 4 ? e : "lhhn"; }();
+    auto level = [&](char c) { return c == 'l' ? plo : c == 'h' ? phi : 0; };
+    auto mk = [](hipStream_t* st, int pr) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, pr); };
+    if ((e = mk(&h->stream, level(prio[1]))) != hipSuccess) return bad(e, "hipStreamCreate");
     for (hipEvent_t* ev : {&h->ev_user, &h->ev_join_out, &h->ev_join_acc})
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
-    for (auto sp : {std::make_pair(&h->s_front, plo), std::make_pair(&h->s_acc, phi), std::make_pair(&h->s_out, 0)})
+    for (auto sp : {std::make_pair(&h->s_front, level(prio[0])), std::make_pair(&h->s_acc, level(prio[2])),
+                    std::make_pair(&h->s_out, level(prio[3]))})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame

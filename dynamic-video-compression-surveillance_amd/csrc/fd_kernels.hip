@@ -72,8 +72,11 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 }
 
 // ------------------------------------------------------------------ front ---
-// Tile: 256 px (64 lanes x 4 px) x 16 rows; 4 waves. Gray halo 2 px / 2 rows,
-// loaded as 66 quads x 20 rows with BORDER_REFLECT_101 at the image edges.
+// Tile: 256 px (64 lanes x 4 px) x 4*NW rows; NW waves, 4 output rows each
+// (interleaved: wave w owns rows w, w+NW, w+2NW, w+3NW). Gray halo 2 px / 2
+// rows, loaded as 66 quads x (4*NW + 4) rows with BORDER_REFLECT_101 at the
+// image edges — taller tiles re-read fewer halo rows (20/16 at NW = 4, 68/64 at
+// NW = 16) at the same registers per lane.
 // The workgroup walks a chunk of the batch's frames in order: the previous
 // blurred gray of its 4x4 px per lane stays in registers (fd:133), and frame
 // t+1's BGR loads are issued as soon as frame t's gray is in LDS, so they fly
@@ -81,7 +84,7 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 // previous batch's gray (gray_in), chunk c > 0 first re-derives frame
 // c*chunk-1's blurred gray (a warm-up pass that emits no mask) — more
 // workgroups in flight for one extra frame read per chunk.
-constexpr int FT_W = 256, FT_H = 16, FT_Q = FT_W / 4 + 2, FT_R = FT_H + 4;
+constexpr int FT_W = 256, FT_Q = FT_W / 4 + 2;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
@@ -94,11 +97,13 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 //   5-tap v   packed u16 lanes (sums <= 16 * 4080 < 2^16), (s + 128) >> 8
 //   threshold |cur - prev| > t per u16 lane as bit 15 of d + (0x7fff - t)
 // The previous blurred gray (fd:133) stays in registers as two u16 pairs.
-__global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
-                                               int chunk, const uint8_t* __restrict__ gray_in,
-                                               uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
-                                               int W, int H, int WW, int ithresh)
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
+                                                   int chunk, const uint8_t* __restrict__ gray_in,
+                                                   uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
+                                                   int W, int H, int WW, int ithresh)
 {
+    constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -116,25 +121,27 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     // quad holding px W-1 may be partial (W % 4): it is loaded in place (frame
     // rows are padded to 3 * gs bytes); quads past it reload the last quad.
     const int xc = x < W ? x : gs - 4;
-    u16x2 pl[FT_H / 4], ph[FT_H / 4];
+    u16x2 pl[4], ph[4];
 #pragma unroll
-    for (int i = 0; i < FT_H / 4; ++i) {
-        const int y = min(y0 + wave + 4 * i, H - 1);
+    for (int i = 0; i < 4; ++i) {
+        const int y = min(y0 + wave + NW * i, H - 1);
         const uint32_t v = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * gs + xc);
         pl[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c010c00u));
         ph[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c02u));
     }
-    // BGR of the 20 halo rows: wave w loads rows w, w+4, ..; lane l its quad l
-    // (12 contiguous bytes). The 2 x 20 halo quads left / right of the tile are
-    // loaded and converted once, by lanes 0..39 of wave 0 (lane 2r + side).
+    // BGR of the FT_R halo rows: wave w loads rows w, w+NW, ..; lane l its quad
+    // l (12 contiguous bytes); rows past FT_R (NW > 4) reload a valid row and
+    // are dropped. The 2 x FT_R halo quads left / right of the tile are loaded
+    // and converted once, by threads 0 .. 2*FT_R-1 (thread 2r + side).
     // Addresses are a uniform frame base + 32-bit per-lane offsets.
-    constexpr int NR = FT_R / 4;
+    constexpr int NR = (FT_R + NW - 1) / NW;
     uint32_t off[NR];
 #pragma unroll
-    for (int j = 0; j < NR; ++j) off[j] = (uint32_t)(reflect1(y0 - 2 + wave + 4 * j, H) * pitch + 3 * xc);
-    const bool halo_wave = __builtin_amdgcn_readfirstlane(wave) == 0;   // scalar branch
-    const bool halo = halo_wave && lane < 2 * FT_R;
-    const int hr = lane >> 1, hs = lane & 1;
+    for (int j = 0; j < NR; ++j)
+        off[j] = (uint32_t)(reflect1(y0 - 2 + min(wave + NW * j, FT_R - 1), H) * pitch + 3 * xc);
+    const bool halo_wave = __builtin_amdgcn_readfirstlane(wave) < (2 * FT_R + 63) / 64;   // scalar branch
+    const bool halo = halo_wave && tid < 2 * FT_R;
+    const int hr = min(tid >> 1, FT_R - 1), hs = tid & 1;
     const int hx = x0 + (hs ? FT_W : -4);
     const uint32_t hoff = (uint32_t)(reflect1(y0 - 2 + min(hr, FT_R - 1), H) * pitch +
                                      3 * (hx >= 0 && hx < W ? hx : xc));
@@ -157,10 +164,12 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     const bool fix_l = x0 == 0;
     const int iW = W - x0 + 4;                    // LDS byte index of px W
     const bool fix_r = iW < 4 * FT_Q;
+    constexpr int FB = 64 * ((FT_R + 63) / 64);   // first thread of the right fix-up (after the left one's)
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
     for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j) sg[wave + 4 * j][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
+        for (int j = 0; j < NR; ++j)
+            if (NR * NW == FT_R || wave + NW * j < FT_R) sg[wave + NW * j][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
         if (halo_wave) {
             const uint32_t gh = gray4_dot(h0, h1, h2);
             if (halo) sg[hr][hs ? FT_Q - 1 : 0] = gh;
@@ -172,9 +181,9 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
                     const uint32_t a = sg[tid][1], b = sg[tid][2];
                     sg[tid][0] = (b & 255) | (((a >> 24) & 255) << 8) | (((a >> 16) & 255) << 16) | (((a >> 8) & 255) << 24);
                 }
-            } else if (tid >= 64 && tid < 64 + FT_R) {
+            } else if (tid >= FB && tid < FB + FT_R) {
                 if (fix_r) {             // px W, W+1 = px W-2, W-3 (later bytes are never read)
-                    uint8_t* row = reinterpret_cast<uint8_t*>(&sg[tid - 64][0]);
+                    uint8_t* row = reinterpret_cast<uint8_t*>(&sg[tid - FB][0]);
                     const uint8_t a = row[iW - 2], b = row[iW - 3];
                     row[iW] = a;
                     if (iW + 1 < 4 * FT_Q) row[iW + 1] = b;
@@ -186,8 +195,8 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
         load(bgr + (size_t)min(t + 1, t_end - 1) * fstride);
 
 #pragma unroll
-        for (int i = 0; i < (FT_R * 64 + 255) / 256; ++i) {
-            const int it = tid + 256 * i;
+        for (int i = 0; i < (FT_R * 64 + NT - 1) / NT; ++i) {
+            const int it = tid + NT * i;
             if (it < FT_R * 64) {
                 const int r = it >> 6, q = it & 63;
                 const uint32_t a = sg[r][q], b = sg[r][q + 1], c = sg[r][q + 2];
@@ -205,8 +214,8 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
 
         uint64_t* mb = mbits + (size_t)t * mstride;
 #pragma unroll
-        for (int i = 0; i < FT_H / 4; ++i) {
-            const int rr = wave + 4 * i, y = y0 + rr;
+        for (int i = 0; i < 4; ++i) {
+            const int rr = wave + NW * i, y = y0 + rr;
             const uint2 a0 = sh[rr][lane], a1 = sh[rr + 1][lane], a2 = sh[rr + 2][lane], a3 = sh[rr + 3][lane],
                         a4 = sh[rr + 4][lane];
             // 16-bit lanes: sum <= 16 * 4080 = 65280, packed adds cannot carry across halves
@@ -238,8 +247,8 @@ __global__ void __launch_bounds__(256) k_front(const uint8_t* __restrict__ bgr, 
     // frame n-1's blurred gray becomes the previous gray of the next batch
     if (t_end == n) {
 #pragma unroll
-        for (int i = 0; i < FT_H / 4; ++i) {
-            const int y = y0 + wave + 4 * i;
+        for (int i = 0; i < 4; ++i) {
+            const int y = y0 + wave + NW * i;
             if (y < H && x < W)
                 *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * gs + x) =
                     __builtin_amdgcn_perm(as_u32(ph[i]), as_u32(pl[i]), 0x06040200u);
@@ -1220,22 +1229,34 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
-                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
+template <int NW>
+static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+                            uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
+    constexpr int FT_H = 4 * NW;
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
-    // chunks: ~1280 workgroups, at least 8 frames per chunk (1080p x 191: 2
-    // chunks, measured best of 1..9 — each extra chunk re-reads a warm-up frame
-    // and adds workgroups competing with the contour filter); DVC_FRONT_WGS /
-    // DVC_FRONT_MIN override for sweeps
-    static const int target = [] { const char* e = getenv("DVC_FRONT_WGS"); return e ? std::max(1, atoi(e)) : 1280; }();
-    int chunks = (target + tx * ty / 2) / (tx * ty);
+    // chunks of the batch: ~5120 waves in flight (1280 workgroups of 4 waves),
+    // at least 8 frames per chunk — each extra chunk re-reads a warm-up frame
+    // and adds waves competing with the contour filter (1080p x 191 at NW = 4:
+    // 2 chunks, measured best of 1..9); DVC_FRONT_WAVES / DVC_FRONT_MIN override
+    static const int target = [] { const char* e = getenv("DVC_FRONT_WAVES"); return e ? std::max(1, atoi(e)) : 5120; }();
+    int chunks = (target / NW + tx * ty / 2) / (tx * ty);
     static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
     chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
-    hipLaunchKernelGGL(k_front, dim3(tx, ty, chunks), dim3(256), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
+    hipLaunchKernelGGL(k_front<NW>, dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
                        gray_out, gs, mbits, g.W, g.H, g.WW, ithresh);
+}
+
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
+{
+    // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16)
+    static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
+    if (nw == 16) launch_front_nw<16>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    else launch_front_nw<4>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
     return hipGetLastError();
 }
 

@@ -424,6 +424,8 @@ def _of_lib():
                                        ctypes.c_double, fp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.oc_update_matrices.argtypes = [fp, fp, fp, ctypes.c_int, ctypes.c_int, fp, ctypes.c_int, ctypes.c_int]
         L.oc_update_flow_box.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
+        L.oc_update_flow_box_sliding.argtypes = [fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp]
+        L.oc_of_set_sliding.argtypes = [ctypes.c_int]
         L._of_ready = True
     return L
 
@@ -485,6 +487,12 @@ def of_compress(bgr: np.ndarray, mask: np.ndarray, quant=100.0) -> np.ndarray:
     H, W = mask.shape
     _of_lib().oc_of_compress(_u8(bgr), 3 * W, _u8(mask), W, H, quant, _u8(out))
     return out
+
+
+def set_sliding(on: bool) -> None:
+    """Box sums of FarnebackUpdateFlow_Blur: OpenCV's incremental (sliding)
+    accumulation (True) or the direct per-pixel sums the HIP kernels use (False)."""
+    _of_lib().oc_of_set_sliding(1 if on else 0)
 
 
 def vote_threshold(alpha: float, L: int) -> int:

@@ -49,6 +49,8 @@ void oc_poly_gauss(int n, double sigma, float* g, float* xg, float* xxg, double*
 void oc_poly_exp(const float* src, int W, int H, int n, double sigma, float* dst);
 void oc_update_matrices(const float* R0, const float* R1, const float* flow, int W, int H, float* M, int y0, int y1);
 void oc_update_flow_box(const float* M, int W, int H, int bs, float* flow);
+void oc_update_flow_box_sliding(const float* M, int W, int H, int bs, float* flow);
+void oc_of_set_sliding(int on);
 int oc_fb_levels(int W, int H, double pyr_scale, int levels);
 void oc_fb_level_poly(const uint8_t* gray, int W, int H, double pyr_scale, int k, int poly_n, double poly_sigma,
                       float* R, int* lw, int* lh);

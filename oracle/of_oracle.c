@@ -294,6 +294,65 @@ void oc_update_flow_box(const float* M, int W, int H, int bs, float* flow)
     free(vs);
 }
 
+/* FarnebackUpdateFlow_Blur exactly as OpenCV 4.11 optflowgf.cpp accumulates
+ * it: a vertical running sum per column (vsum, double) initialised with row 0
+ * times (m + 2) — a FLOAT product — plus rows 1..m-1, then per row
+ * vsum += (float)(M[y+m] - M[y-m-1]) (the difference of two floats is rounded
+ * to float before the double add); replicated borders of m + 1 columns; a
+ * horizontal running sum per row initialised with vsum[0] * (m + 2) plus
+ * columns 1..m-1, then g += vsum[x+m] - vsum[x-m-1] (double). Same solve.
+ * Selected by oc_of_set_sliding(1); the measured difference to the direct sums
+ * is reported by tests/test_of_sliding.py. */
+void oc_update_flow_box_sliding(const float* M, int W, int H, int bs, float* flow)
+{
+    const int m = bs / 2;
+    const double scale = 1. / (bs * bs);
+    double* buf = (double*)malloc(sizeof(double) * 5 * (size_t)(W + 2 * m + 2));
+    double* vsum = buf + (m + 1) * 5;
+    const size_t rs = (size_t)W * 5;
+    const float* srow0 = M;
+    for (size_t x = 0; x < rs; ++x) vsum[x] = srow0[x] * (m + 2);
+    for (int y = 1; y < m; ++y) {
+        srow0 = M + (size_t)(y < H - 1 ? y : H - 1) * rs;
+        for (size_t x = 0; x < rs; ++x) vsum[x] += srow0[x];
+    }
+    for (int y = 0; y < H; ++y) {
+        srow0 = M + (size_t)(y - m - 1 > 0 ? y - m - 1 : 0) * rs;
+        const float* srow1 = M + (size_t)(y + m < H - 1 ? y + m : H - 1) * rs;
+        for (size_t x = 0; x < rs; ++x) vsum[x] += srow1[x] - srow0[x];
+        for (int x = 0; x < (m + 1) * 5; ++x) {
+            vsum[-1 - x] = vsum[4 - x];
+            vsum[W * 5 + x] = vsum[W * 5 + x - 5];
+        }
+        double g11 = vsum[0] * (m + 2), g12 = vsum[1] * (m + 2), g22 = vsum[2] * (m + 2);
+        double h1 = vsum[3] * (m + 2), h2 = vsum[4] * (m + 2);
+        for (int x = 1; x < m; ++x) {
+            g11 += vsum[x * 5];
+            g12 += vsum[x * 5 + 1];
+            g22 += vsum[x * 5 + 2];
+            h1 += vsum[x * 5 + 3];
+            h2 += vsum[x * 5 + 4];
+        }
+        float* fl = flow + (size_t)y * W * 2;
+        for (int x = 0; x < W; ++x) {
+            g11 += vsum[(x + m) * 5] - vsum[(x - m) * 5 - 5];
+            g12 += vsum[(x + m) * 5 + 1] - vsum[(x - m) * 5 - 4];
+            g22 += vsum[(x + m) * 5 + 2] - vsum[(x - m) * 5 - 3];
+            h1 += vsum[(x + m) * 5 + 3] - vsum[(x - m) * 5 - 2];
+            h2 += vsum[(x + m) * 5 + 4] - vsum[(x - m) * 5 - 1];
+            const double g11_ = g11 * scale, g12_ = g12 * scale, g22_ = g22 * scale;
+            const double h1_ = h1 * scale, h2_ = h2 * scale;
+            const double idet = 1. / (g11_ * g22_ - g12_ * g12_ + 1e-3);
+            fl[x * 2] = (float)((g11_ * h2_ - g12_ * h1_) * idet);
+            fl[x * 2 + 1] = (float)((g22_ * h1_ - g12_ * h2_) * idet);
+        }
+    }
+    free(buf);
+}
+
+static int oc_sliding = 0;
+void oc_of_set_sliding(int on) { oc_sliding = on; }
+
 /* Pyramid level geometry of calcOpticalFlowFarneback (min_size 32). */
 int oc_fb_levels(int W, int H, double pyr_scale, int levels)
 {
@@ -357,7 +416,8 @@ void oc_farneback(const uint8_t* prev, const uint8_t* next, int W, int H, double
         float* M = (float*)malloc(sizeof(float) * 5 * (size_t)w * h);
         oc_update_matrices(R0, R1, flow, w, h, M, 0, h);
         for (int it = 0; it < iterations; ++it) {
-            oc_update_flow_box(M, w, h, winsize, flow);
+            if (oc_sliding) oc_update_flow_box_sliding(M, w, h, winsize, flow);
+            else oc_update_flow_box(M, w, h, winsize, flow);
             if (it < iterations - 1) oc_update_matrices(R0, R1, flow, w, h, M, 0, h);
         }
         free(M); free(R0); free(R1);

@@ -1,0 +1,46 @@
+"""How far the OF box-sum order matters.
+
+OpenCV's FarnebackUpdateFlow_Blur accumulates the 9x9 box sums incrementally
+(a vertical running double sum per column fed with float row differences, a
+horizontal running double sum per row; oracle/of_oracle.c
+oc_update_flow_box_sliding); the oracle's default and the HIP kernels use
+direct per-pixel double sums. The running sums carry rounding residue along a
+column or row (after a textured region the residue of its large values stays
+in the sum over a flat one), so flow values differ — up to ~0.4 px where G is
+near singular — but the thresholded, voted, morphology-closed rectangle mask
+and the compressed frames, i.e. the reference's outputs, are identical on every
+golden case (the 1080p measurement in DESIGN.md §2 adds one raw-mask bit flip
+in 14.5 M px over 7 frames, no output change).
+"""
+import numpy as np
+import pytest
+
+from tests.golden.cases_of import CASES
+
+
+def _run(oracle, frames, kw, sliding):
+    oracle.set_sliding(sliding)
+    try:
+        H, W = frames.shape[1:3]
+        o = oracle.OracleOF(W, H, **kw)
+        o.prime(frames[0])
+        out = []
+        for f in frames[1:]:
+            mk, cp, fl = o.step(f)
+            out.append((mk, cp, fl, o.plane(0)))
+        o.close()
+        return out
+    finally:
+        oracle.set_sliding(False)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_sliding_order_same_outputs(oracle_lib, name):
+    mk, kw = CASES[name]
+    frames = mk()
+    a, b = _run(oracle_lib, frames, kw, False), _run(oracle_lib, frames, kw, True)
+    for t, (x, y) in enumerate(zip(a, b)):
+        assert np.array_equal(x[0], y[0]), (name, "rectangle mask", t)
+        assert np.array_equal(x[1], y[1]), (name, "compressed", t)
+    # the flow itself is not bit-identical (documented, not asserted small)
+    assert max(float(np.abs(x[2] - y[2]).max()) for x, y in zip(a, b)) < 1.0

@@ -47,7 +47,7 @@ int main(int argc, char** argv)
     CK(hipMalloc(&gray1, N));
     CK(hipMalloc(&gtmp, N));
     CK(hipMalloc(&tmp32, 4 * N));
-    CK(hipMalloc(&acc, N));
+    CK(hipMalloc(&acc, N + 4 * (size_t)W));
     CK(hipMalloc(&ov, F * n));
     CK(hipMalloc(&cp, F * n));
     CK(hipMalloc(&stats, 8 * 4 * 64));
@@ -60,23 +60,27 @@ int main(int argc, char** argv)
     for (int i = 0; i < 10; ++i) CK(hipMalloc(ptrs[i], sz[i]));
     CK(hipMemset(c.gpar, 0, sz[6]));
     c.stats = stats;
-    const int B = 4, SW = (W / B + 63) / 64;
+    const int B = 4, NBX = (W + B - 1) / B, NBY = (H + B - 1) / B, SW = (NBX + 63) / 64, gs = (W + 3) & ~3;
     uint64_t *dblk, *rblk, *sbits;
-    CK(hipMalloc(&dblk, 8 * (size_t)H * g.WW * n));
-    CK(hipMalloc(&rblk, 8 * (size_t)H * g.WW * n));
-    CK(hipMalloc(&sbits, 8 * (size_t)(H / B) * SW * n));
+    CK(hipMalloc(&dblk, 2 * (size_t)NBX * NBY * n));
+    CK(hipMalloc(&rblk, 2 * (size_t)NBX * NBY * n));
+    CK(hipMalloc(&sbits, 8 * (size_t)NBY * SW * n));
     dvc::GaussTaps kp{};
     kp.n = 25;
     // taps for (25, 30.0) as the handle computes them (dvc_gaussian_taps_q8)
     const uint16_t t25[25] = {10, 10, 10, 10, 10, 10, 10, 11, 10, 11, 10, 11, 10, 11, 10, 11, 10, 11, 10, 10, 10, 10, 10, 10, 10};
     for (int i = 0; i < 25; ++i) kp.t[i] = t25[i];
-    CK(dvc::launch_prime(frames, 3 * W, gtmp, tmp32, gray0, W, H, kp, nullptr));
+    CK(dvc::launch_prime(frames, 3 * W, gtmp, tmp32, gray0, W, H, gs, kp, nullptr));
     dvc::BackArgs a{};
     a.g = g;
     a.bgr = frames + F;
     a.pitch = 3 * W;
     a.fstride = F;
     a.acc = acc;
+    a.ap = NBX * B;
+    a.B = B;
+    a.NBX = NBX;
+    a.NBY = NBY;
     a.overlay = ov;
     a.compressed = cp;
     a.opitch = 3 * W;
@@ -86,7 +90,7 @@ int main(int argc, char** argv)
     a.rblk = rblk;
     a.sbits = sbits;
     a.SW = SW;
-    a.sstride = (size_t)(H / B) * SW;
+    a.sstride = (size_t)NBY * SW;
     a.n = n;
     a.ksize = 7;
     a.anchor = 3;
@@ -100,21 +104,25 @@ int main(int argc, char** argv)
         for (int j = 0; j < 4; ++j)
             a.M.m[k * 4 + j] = a.M.mt[j * 4 + k] = (float)((k == 0 ? std::sqrt(0.25) : std::sqrt(0.5)) * std::cos(M_PI * (2 * j + 1) * k / 8.0));
     a.stats = stats;
+    unsigned long long* err;
+    CK(hipMalloc(&err, 8));
+    CK(hipMemset(err, 0xff, 8));
+    a.err = err;
     double tf = 0, tc = 0, tb = 0;
     for (int r = 0; r < reps; ++r) {
         CK(hipDeviceSynchronize());
         auto t0 = std::chrono::steady_clock::now();
         // rep 0 starts from the 25x25-blurred prime gray (a near-full first mask);
         // later reps continue from the previous rep's last gray like a feed would
-        CK(dvc::launch_front(frames + F, 3 * W, F, n, (r & 1) ? gray1 : gray0, (r & 1) ? gray0 : gray1, c.mbits, g,
+        CK(dvc::launch_front(frames + F, 3 * W, F, n, (r & 1) ? gray1 : gray0, (r & 1) ? gray0 : gray1, gs, c.mbits, g,
                              0, nullptr));
         CK(hipDeviceSynchronize());
         auto t1 = std::chrono::steady_clock::now();
         CK(dvc::launch_ccl(c, g, n, 1000, nullptr));
         CK(hipDeviceSynchronize());
         auto t2 = std::chrono::steady_clock::now();
-        CK(dvc::launch_accumulate(a, 4, nullptr));
-        CK(dvc::launch_out(a, 4, nullptr));
+        CK(dvc::launch_accumulate(a, nullptr));
+        CK(dvc::launch_out(a, nullptr));
         CK(hipDeviceSynchronize());
         auto t3 = std::chrono::steady_clock::now();
         if (r > 0) {
