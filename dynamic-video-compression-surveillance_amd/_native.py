@@ -26,6 +26,7 @@ DVC_FLAG_DEVICE_PTRS = 0x1
 DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
 DVC_FLAG_JOIN_STREAM = 0x8
+DVC_FLAG_OF_DIRECT_SUMS = 0x10
 
 PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
 OF_PLANE_RAW, OF_PLANE_SMOOTH, OF_PLANE_MORPH, OF_PLANE_RECT, OF_PLANE_GRAY = range(5)

@@ -146,6 +146,7 @@ struct dvc_of {
     uint8_t *h_in = nullptr, *h_mask = nullptr, *h_cp = nullptr;
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
+    unsigned int epoch = 0;   // k_flow_scan launches so far (hand-off flags carry it)
 };
 
 static void of_free(dvc_of* h)
@@ -190,6 +191,15 @@ static hipError_t of_sync_all(dvc_of* h)
     for (hipStream_t st : {h->s_flow, h->s_mask})
         if (e == hipSuccess && st) e = hipStreamSynchronize(st);
     return e;
+}
+
+// After a sync: did a k_flow_scan hand-off wait time out? (never in a correct run)
+static int of_check_abort(dvc_of* h)
+{
+    unsigned int ab = 0;
+    HIP_OK(hipMemcpy(&ab, h->b.scan_abort, 4, hipMemcpyDeviceToHost));
+    if (ab) return fail(DVC_E_HIP, "k_flow_scan: a strip hand-off wait timed out");
+    return DVC_OK;
 }
 
 template <typename T>
@@ -256,6 +266,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     g.box_scale = 1. / (p.winsize * p.winsize);
     g.up = (float)(1. / p.pyr_scale);
     g.flow_thr = p.flow_threshold;
+    g.sliding = !(p.flags & DVC_FLAG_OF_DIRECT_SUMS);
     poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
     dvc_host::dct_matrix(8, h->M);
 
@@ -364,11 +375,25 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         {(void**)&b.roots, 4 * H * CAP * mb},
         {(void**)&b.nroots, 4 * (size_t)mb},
         {(void**)&b.stats, 8 * 4 * 64},
+        {(void**)&b.scan_ctr, 4},
+        {(void**)&b.scan_abort, 4},
     };
     for (auto& a : allocs)
         if ((e = of_alloc(h, a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
     if (p.flags & DVC_FLAG_KEEP_PLANES)
         if ((e = of_alloc(h, &b.dbg_flow, 8 * N)) != hipSuccess) return bad(e, "hipMalloc");
+    if (g.sliding) {   // k_flow_scan hand-off state, sized for the largest level
+        size_t cells = 0, strips = 0;
+        for (int k = 0; k <= L; ++k) {
+            const size_t sk = dvc::of_scan_strips(h->lv[k].w);
+            cells = std::max(cells, sk * h->lv[k].h);
+            strips = std::max(strips, sk);
+        }
+        if ((e = of_alloc(h, &b.scan_g, 8 * 5 * cells * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = of_alloc(h, &b.scan_flags, 8 * strips * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = hipMemset(b.scan_flags, 0, 8 * strips * mb)) != hipSuccess) return bad(e, "hipMemset");
+    }
+    if ((e = hipMemset(b.scan_abort, 0, 4)) != hipSuccess) return bad(e, "hipMemset");
     uint8_t vt[256];
     std::memset(vt, 0, sizeof(vt));
     for (int l = 1; l <= p.window; ++l) vt[l] = (uint8_t)vote_threshold(p.alpha_fraction, l);
@@ -440,9 +465,9 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow));
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow, &h->epoch));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_flow));
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow));
+    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_flow));
         h->ev_used += 2;
@@ -512,7 +537,7 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
         }
     }
     HIP_OK(of_join_user(h));
-    return DVC_OK;
+    return devp ? DVC_OK : of_check_abort(h);
 }
 
 extern "C" {
@@ -533,7 +558,7 @@ int dvc_of_sync(dvc_of* h)
     if (!h) return fail(DVC_E_INVALID, "NULL handle");
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_sync_all(h));
-    return DVC_OK;
+    return of_check_abort(h);
 }
 
 int dvc_of_get_stats(dvc_of* h, dvc_of_stats* out)

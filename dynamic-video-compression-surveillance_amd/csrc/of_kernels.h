@@ -63,6 +63,7 @@ struct OfGeom {
     double box_scale;  // 1 / (winsize * winsize)
     float up;          // (float)(1 / pyr_scale)
     float flow_thr;
+    int sliding;       // box sums in OpenCV's running order (k_flow_scan) / direct per pixel (k_flow)
     PolyCoef pc;
 };
 
@@ -85,6 +86,11 @@ struct OfBufs {
     uint32_t* nroots;      // n
     float* dbg_flow;       // nullable: final flow of the batch's last frame (W*H*2)
     unsigned long long* stats;  // 64 slots x 4: frames, motion px, components, static blocks
+    // k_flow_scan (sliding box sums): strip hand-off state
+    double* scan_g;                // n x strips x h x 5 running sums (sized for the largest level)
+    unsigned long long* scan_flags;   // n x strips
+    unsigned int* scan_ctr;        // work-item counter
+    unsigned int* scan_abort;      // a hand-off wait timed out
 };
 
 struct OfOutArgs {
@@ -107,7 +113,9 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 // Farneback levels k_hi down to k_lo (L..0 in total, coarse to fine) for frames
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s);
+                          hipStream_t s, unsigned int* epoch);
+// strips of the sliding-sum kernel across a level of width w (at most: strips of 32 columns)
+inline int of_scan_strips(int w) { return (w + 31) / 32; }
 // vote (frames in order) -> close/open -> 8-CC bounding boxes -> rectangle mask
 hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s);
 // compress_with_motion (of:151-183) + the mask bytes

@@ -31,6 +31,8 @@
 
 #include <algorithm>
 #include <numeric>
+#include <cstdlib>
+#include <cstring>
 
 #include "dvc_device.h"
 #include "of_kernels.h"
@@ -581,6 +583,353 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
     }
 }
 
+// ------------------------------------------------------ flow: sliding sums --
+// FarnebackUpdateFlow_Blur with OpenCV's own accumulation order
+// (optflowgf.cpp; oracle/of_oracle.c oc_update_flow_box_sliding): per column a
+// vertical running double sum fed with float row differences, per row a
+// horizontal running double sum — recurrences whose rounding is part of the
+// result, so they are walked in order. A work item is one strip of SC_W
+// columns of one frame: its workgroup walks the level's rows in blocks of SC_R
+//   1. FarnebackUpdateMatrices of the block's new M rows over the strip's
+//      columns + the box halo (m + 1 left, m right), into an LDS ring of rows;
+//   2. the vertical recurrence of every (column, channel) of the strip for the
+//      block's rows, the state in registers across blocks, the sums in LDS;
+//   3. the horizontal recurrence of every (row, channel) across the strip's
+//      columns, started from the state the strip to its left published for
+//      that row (strip 0: OpenCV's (m + 2) vsum[0] + vsum[1..m-1] start);
+//      the state after the strip's last column is published for the right
+//      neighbour (payload, release fence, flag — one wave);
+//   4. flow = G^-1 h per pixel (or |flow| > thr bits on the finest level's
+//      last iteration).
+// Strips of a frame form a wavefront: strip s waits, block by block, for
+// strip s-1's published state. Items are dequeued in (frame, strip) order from
+// a counter, so the strip an item waits on was taken earlier by a running
+// workgroup: no residency assumption, no deadlock. A wait that ever exceeds
+// ~1 s sets `abort` (reported by the host as an error) instead of hanging.
+struct ScanArgs {
+    FlowArgs f;
+    int S;                       // strips across the level
+    double* gpub;                // n x S x h x 5: state after each strip's last column, per row
+    unsigned long long* flags;   // n x S: (epoch << 32) | row blocks published
+    unsigned int* next;          // work-item counter, zeroed before the launch
+    unsigned int* abort;         // a wait timed out (never in a correct run)
+    unsigned int epoch;          // launch number (flags of older launches compare lower)
+};
+
+// strip width SW (columns) and rows per block RB; LDS: the M ring (RB + 2m + 1
+// rows of SW + 2m + 1 columns x 5 floats), the block's vertical sums (RB rows x
+// SW + 2m + 1 columns x 5 doubles) and its horizontal sums (RB x SW x 5 doubles)
+__host__ __device__ constexpr int scan_ring(int rb, int m) { return rb + 2 * m + 1; }
+__host__ __device__ constexpr int scan_nc(int sw, int m) { return sw + 2 * m + 1; }
+inline size_t scan_lds_bytes(int sw, int rb, int m)
+{
+    return (size_t)scan_ring(rb, m) * scan_nc(sw, m) * 5 * 4 + (size_t)rb * scan_nc(sw, m) * 5 * 8 +
+           (size_t)rb * sw * 5 * 8;
+}
+
+// M of FarnebackUpdateMatrices (oc_update_matrices) at MQ positions, each
+// (x, y) inside the level; results to LDS at dst[u] (5 floats). All loads of
+// the MQ positions are issued before any of their arithmetic.
+template <int MQ>
+__device__ __forceinline__ void mat_positions(const FlowArgs& A, const float* __restrict__ R0,
+                                              const float* __restrict__ R1, const float* src, const int (&xs)[MQ],
+                                              const int (&ys)[MQ], const bool (&ok)[MQ], float* const (&dst)[MQ])
+{
+    const OfGeom& g = A.g;
+    const int w = A.lv.w, h = A.lv.h;
+    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
+    float dxv[MQ], dyv[MQ], r0v[MQ][5];
+#pragma unroll
+    for (int u = 0; u < MQ; ++u) {
+        const uint32_t pix = (uint32_t)(ys[u] * w + xs[u]);
+        dxv[u] = 0.f;
+        dyv[u] = 0.f;
+        if (A.src_mode == 2) {   // uniform
+            const float2 f = *reinterpret_cast<const float2*>(src + 2u * pix);
+            dxv[u] = f.x;
+            dyv[u] = f.y;
+        } else if (A.src_mode == 1) {
+            const LinTap ty = A.lv.uy[ys[u]], tx = A.lv.ux[xs[u]];
+            const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
+            const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
+            float v[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float t0 = ra[tx.s0 * 2 + c] * tx.w0 + ra[tx.s1 * 2 + c] * tx.w1;
+                const float t1 = rb[tx.s0 * 2 + c] * tx.w0 + rb[tx.s1 * 2 + c] * tx.w1;
+                v[c] = t0 * ty.w0 + t1 * ty.w1;
+            }
+            dxv[u] = v[0] * g.up;
+            dyv[u] = v[1] * g.up;
+        }
+        const float* r0 = R0 + 5u * pix;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) r0v[u][c] = r0[c];
+    }
+    float pq[MQ][20], fxv[MQ], fyv[MQ];
+    bool inb[MQ];
+#pragma unroll
+    for (int u = 0; u < MQ; ++u) {
+        float fx = (float)xs[u] + dxv[u], fy = (float)ys[u] + dyv[u];
+        const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
+        fxv[u] = fx - (float)x1;
+        fyv[u] = fy - (float)y1;
+        inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
+        const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
+        const float* p = R1 + 5u * (uint32_t)(y1c * w + x1c);
+        const float* q = p + 5u * (uint32_t)w;
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            pq[u][c] = p[c];
+            pq[u][10 + c] = q[c];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < MQ; ++u) {
+        if (!ok[u]) continue;
+        const int x = xs[u], y = ys[u];
+        const float dx = dxv[u], dy = dyv[u], fx = fxv[u], fy = fyv[u];
+        const float* r0 = r0v[u];
+        const float* p = pq[u];
+        const float* q = pq[u] + 10;
+        f32x2 R23, R45;
+        float r6;
+        const f32x2 R0_01 = {r0[0], r0[1]}, R0_23 = {r0[2], r0[3]};
+        if (inb[u]) {
+            const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+            const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
+            const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
+            const f32x2 Q01 = {q[0], q[1]}, Q23 = {q[2], q[3]}, Q56 = {q[5], q[6]}, Q78 = {q[7], q[8]};
+            R23 = A00 * P01 + A01 * P56 + A10 * Q01 + A11 * Q56;
+            R45 = A00 * P23 + A01 * P78 + A10 * Q23 + A11 * Q78;
+            r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
+            R45 = (R0_23 + R45) * (f32x2)0.5f;
+            r6 = (r0[4] + r6) * 0.25f;
+        } else {
+            R23 = (f32x2)0.f;
+            R45 = R0_23;
+            r6 = r0[4] * 0.5f;
+        }
+        R23 = (R0_01 - R23) * (f32x2)0.5f;
+        R23 = R23 + ((f32x2){R45.x, r6} * (f32x2)dy + (f32x2){r6, R45.y} * (f32x2)dx);
+        if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
+            const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
+                                (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+            R23 = R23 * (f32x2)scale;
+            R45 = R45 * (f32x2)scale;
+            r6 *= scale;
+        }
+        float* M = dst[u];
+        const f32x2 G = R45 * R45 + (f32x2)(r6 * r6);
+        const f32x2 Hh = (f32x2){R45.x, r6} * (f32x2)R23.x + (f32x2){r6, R45.y} * (f32x2)R23.y;
+        M[0] = G.x;
+        M[1] = (R45.x + R45.y) * r6;
+        M[2] = G.y;
+        M[3] = Hh.x;
+        M[4] = Hh.y;
+    }
+}
+
+// Hand-offs between strips use agent-scope relaxed atomics for payload and
+// flag (sc1: coherent across XCDs without cache maintenance) — no agent-scope
+// fence: an acquire would invalidate the XCD's L2 under every other workgroup
+// and a release would write it back (measured: 20 us per row block with them).
+// The producer orders payload before flag by draining its stores (vmcnt(0));
+// the consumer's payload loads are issued after the flag load returned.
+__device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long long* flag, unsigned long long want)
+{
+    unsigned spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (__hip_atomic_load(S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {      // ~1 s: never in a correct run
+            __hip_atomic_store(S.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    asm volatile("" ::: "memory");
+    return true;
+}
+
+template <int SW, int RB>
+__device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, double* sG, int* s_alive)
+{
+    const FlowArgs& A = S.f;
+    const OfGeom& g = A.g;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w = A.lv.w, h = A.lv.h, m = g.m;
+    const int RING = scan_ring(RB, m), NC = scan_nc(SW, m);
+    const int X0 = s * SW, X1 = min(X0 + SW, w), CX0 = X0 - m - 1, nx = X1 - X0;
+    const size_t lvpx = (size_t)w * h;
+    const long long a = A.a0 + t;
+    const float* __restrict__ R0 = A.lv.R + (size_t)ring(a - 1, g.RS) * lvpx * 5;
+    const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
+    const float* src = A.src ? A.src + (size_t)t * (A.src_mode == 1 ? (size_t)A.sw * A.sh : lvpx) * 2 : nullptr;
+    float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
+    unsigned long long* myflag = S.flags + (size_t)t * S.S + s;
+    const unsigned long long* lflag = s > 0 ? myflag - 1 : nullptr;
+    double* gp_mine = S.gpub + ((size_t)t * S.S + s) * (size_t)h * 5;
+    const double* gp_left = s > 0 ? gp_mine - (size_t)h * 5 : nullptr;
+    const unsigned long long ep = (unsigned long long)S.epoch << 32;
+    // vertical chains of this thread: (column, channel) ch = tid + 256 k
+    const int nch = NC * 5;
+    constexpr int KV = (scan_nc(SW, OF_MAX_BOX_M) * 5 + 255) / 256;
+    double vsum[KV];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) vsum[k] = 0.0;
+    auto mrow = [&](int r) { return sM + (size_t)(r % RING) * NC * 5; };
+    for (int y0 = 0; y0 < h; y0 += RB) {
+        const int yb = y0 / RB, nrow = min(RB, h - y0);
+        // 1. M rows [rlo, rhi] (block 0 also rows 0..m-1 for the start)
+        const int rlo = y0 == 0 ? 0 : (y0 + m <= h - 1 ? y0 + m : h);
+        const int rhi = min(y0 + RB - 1 + m, h - 1);
+        const int npos = rhi >= rlo ? (rhi - rlo + 1) * NC : 0;
+        constexpr int MQ = 3;
+        for (int q0 = tid; q0 < npos; q0 += 256 * MQ) {
+            int xs[MQ], ys[MQ];
+            bool ok[MQ];
+            float* d[MQ];
+#pragma unroll
+            for (int u = 0; u < MQ; ++u) {
+                const int idx = q0 + 256 * u;
+                ok[u] = idx < npos;
+                const int ii = ok[u] ? idx : 0;
+                const int r = rlo + ii / NC, j = ii - (ii / NC) * NC;
+                xs[u] = min(max(CX0 + j, 0), w - 1);
+                ys[u] = r;
+                d[u] = mrow(r) + j * 5;
+            }
+            mat_positions<MQ>(A, R0, R1, src, xs, ys, ok, d);
+        }
+        __syncthreads();
+        // 2. vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ch = tid + 256 * k;
+            if (ch >= nch) continue;
+            const int j = ch / 5, c = ch - 5 * j;
+            if (y0 == 0) {   // vsum = row0 * (m+2) (a float product) + rows 1..m-1
+                vsum[k] = (double)(mrow(0)[j * 5 + c] * (float)(m + 2));
+                for (int r = 1; r < m; ++r) vsum[k] += (double)mrow(min(r, h - 1))[j * 5 + c];
+            }
+            for (int i = 0; i < nrow; ++i) {
+                const int y = y0 + i;
+                const float dd = mrow(min(y + m, h - 1))[j * 5 + c] - mrow(max(y - m - 1, 0))[j * 5 + c];
+                vsum[k] += (double)dd;
+                sV[((size_t)i * NC + j) * 5 + c] = vsum[k];
+            }
+        }
+        __syncthreads();
+        // 3a. the horizontal increments vsum[x+m] - vsum[x-m-1] (independent: all
+        // threads) into sG; meanwhile thread 0 waits for the left strip's block
+        if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
+        for (int e = tid; e < nrow * SW * 5; e += 256) {
+            const int i = e / (SW * 5), rem = e - i * (SW * 5), xl = rem / 5, c = rem - 5 * xl;
+            if (xl >= nx) continue;
+            const double* v = sV + (size_t)i * NC * 5 + c;
+            const int x = X0 + xl;
+            sG[e] = v[(x + m - CX0) * 5] - v[(x - m - 1 - CX0) * 5];
+        }
+        __syncthreads();
+        // 3b. the running sums, lanes (row i, channel c); loads batched ahead of
+        // the dependent adds; the state after the last column goes to the right
+        if (tid < nrow * 5) {
+            const int i = tid / 5, c = tid - 5 * i;
+            const double* v = sV + (size_t)i * NC * 5 + c;
+            double acc;
+            if (s == 0) {
+                acc = v[(0 - CX0) * 5] * (double)(m + 2);
+                for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
+            } else {
+                acc = __hip_atomic_load(gp_left + (size_t)(y0 + i) * 5 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            double* gr = sG + (size_t)i * SW * 5 + c;
+            constexpr int U = 8;
+            int xl = 0;
+            for (; xl + U <= nx; xl += U) {
+                double dv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) dv[u] = gr[(xl + u) * 5];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    acc += dv[u];
+                    gr[(xl + u) * 5] = acc;
+                }
+            }
+            for (; xl < nx; ++xl) {
+                acc += gr[xl * 5];
+                gr[xl * 5] = acc;
+            }
+            if (s + 1 < S.S)
+                __hip_atomic_store(gp_mine + (size_t)(y0 + i) * 5 + c, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s + 1 < S.S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the payload stores have landed
+        }
+        __syncthreads();
+        if (s + 1 < S.S && tid == 0)
+            __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // 4. flow = G^-1 h per pixel of the block (a wave = 64 / SW rows of SW columns)
+        for (int e = tid; e < RB * SW; e += 256) {
+            const int i = e / SW, xl = e - i * SW;
+            const int y = y0 + i, x = X0 + xl;
+            const bool act = i < nrow && xl < nx;
+            float fxo = 0.f, fyo = 0.f;
+            if (act) {
+                const double* gg = sG + (size_t)(i * SW + xl) * 5;
+                const double g11 = gg[0] * g.box_scale, g12 = gg[1] * g.box_scale, g22 = gg[2] * g.box_scale;
+                const double h1 = gg[3] * g.box_scale, h2 = gg[4] * g.box_scale;
+                const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+                fxo = (float)((g11 * h2 - g12 * h1) * idet);
+                fyo = (float)((g22 * h1 - g12 * h2) * idet);
+            }
+            if (!A.last) {
+                if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fxo, fyo);
+            } else {
+                const float mag = sqrtf(fxo * fxo + fyo * fyo);   // of:82-83
+                const unsigned long long word = __ballot(act && mag > g.flow_thr);
+                uint64_t* mr = A.mring + (size_t)ring(a, g.RB) * h * g.WW;
+                if constexpr (SW == 64) {
+                    if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
+                } else {   // SW = 32: lanes 0-31 row i, 32-63 row i+1, each half a mask word
+                    uint32_t* mr32 = reinterpret_cast<uint32_t*>(mr);
+                    const int half = (X0 >> 5) & 1;
+                    if ((lane & 31) == 0 && i < nrow) {
+                        mr32[((size_t)y * g.WW + (X0 >> 6)) * 2 + half] = (uint32_t)(word >> (lane & 32));
+                        if (half == 0 && X0 + 32 >= w) mr32[((size_t)y * g.WW + (X0 >> 6)) * 2 + 1] = 0u;
+                    }
+                }
+                if (A.dbg_flow && t == A.n - 1 && act)
+                    *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
+            }
+        }
+        __syncthreads();
+        if (!*s_alive) break;   // uniform (read after the barrier): an aborted launch drains
+    }
+    (void)wave;
+}
+
+template <int SW, int RB>
+__global__ void __launch_bounds__(256) k_flow_scan(ScanArgs S)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_s[];
+    const int m = S.f.g.m;
+    double* sV = lds_s;
+    double* sG = sV + (size_t)RB * scan_nc(SW, m) * 5;
+    float* sM = reinterpret_cast<float*>(sG + (size_t)RB * SW * 5);
+    __shared__ int item, alive;
+    const int total = S.S * S.f.n;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            item = (int)atomicAdd(S.next, 1u);
+            alive = 1;
+        }
+        __syncthreads();
+        const int it = item;
+        __syncthreads();
+        if (it >= total) break;
+        scan_strip<SW, RB>(S, it / S.S, it % S.S, sM, sV, sG, &alive);
+    }
+}
+
 // -------------------------------------------------------------------- vote --
 // of:84-86: count of the last L = min(frames, window) raw masks (the deque),
 // smoothed = count >= vthr[L]. One lane per 16 px (a u16 of a mask word), the
@@ -1031,9 +1380,14 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 }
 
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s)
+                          hipStream_t s, unsigned int* epoch)
 {
     a0 = reduce_frame(g, a0);
+    static const int cus = [] {
+        int dev = 0, c = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 256;
+        return c;
+    }();
     const size_t lds = std::max((size_t)(FL_H + 2 * g.m) * (FL_W + 2 * g.m) * 5 * 4,
                                 (size_t)FL_H * (FL_W + 2 * g.m) * 5 * 8);
     for (int k = k_hi; k >= k_lo; --k) {
@@ -1061,8 +1415,36 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.dst = A.last ? nullptr : L.flow[it & 1];
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
-            if (g.m == 4) hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
-            else hipLaunchKernelGGL(k_flow<0>, grid, dim3(256), lds, s, A);
+            if (g.sliding) {   // OpenCV's running box sums: strip wavefront
+                // strip width x rows per block: 64 x 8 (measured best of 32/64 x 8/16 at 1080p;
+                // DVC_OF_SCAN = "32x8", "32x16", "64x16" for sweeps)
+                static const int scan_cfg = [] {
+                    const char* e = getenv("DVC_OF_SCAN");
+                    return !e ? 1 : !strcmp(e, "32x8") ? 0 : !strcmp(e, "32x16") ? 2 : !strcmp(e, "64x16") ? 3 : 1;
+                }();
+                const int sw = scan_cfg & 1 ? 64 : 32, rb = scan_cfg & 2 ? 16 : 8;
+                ScanArgs S{};
+                S.f = A;
+                S.S = (L.w + sw - 1) / sw;
+                S.gpub = b.scan_g;
+                S.flags = b.scan_flags;
+                S.next = b.scan_ctr;
+                S.abort = b.scan_abort;
+                S.epoch = ++*epoch;
+                hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4, s);
+                if (e != hipSuccess) return e;
+                const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
+                const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
+                const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
+                if (scan_cfg == 0) hipLaunchKernelGGL((k_flow_scan<32, 8>), dim3(grid_s), dim3(256), lds_b, s, S);
+                else if (scan_cfg == 1) hipLaunchKernelGGL((k_flow_scan<64, 8>), dim3(grid_s), dim3(256), lds_b, s, S);
+                else if (scan_cfg == 2) hipLaunchKernelGGL((k_flow_scan<32, 16>), dim3(grid_s), dim3(256), lds_b, s, S);
+                else hipLaunchKernelGGL((k_flow_scan<64, 16>), dim3(grid_s), dim3(256), lds_b, s, S);
+            } else if (g.m == 4) {
+                hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
+            } else {
+                hipLaunchKernelGGL(k_flow<0>, grid, dim3(256), lds, s, A);
+            }
         }
     }
     return hipGetLastError();

@@ -22,11 +22,14 @@ from . import _native as N
 
 def derive_of_params(width: int, height: int, flow_threshold: float = 0.5, alpha_fraction: float = 0.2,
                      window_size: int = 30, morph_kernel: int = 2, quantization_level: float = 100.0,
-                     flags: int = 0) -> N.OfParams:
+                     flags: int = 0, direct_sums: bool = False) -> N.OfParams:
     """dvc_of_params from the reference kwargs of ``temporal_smoothing_flow``
     (of:29-31) and the arguments it hard-codes: Farneback (0.3, 2, 9, 2, 5, 1.1,
-    0) at of:72-81, ``QTY_aggressive`` = 100 at of:138."""
+    0) at of:72-81, ``QTY_aggressive`` = 100 at of:138. ``direct_sums``: direct
+    per-pixel box sums instead of OpenCV's running sums (the default)."""
     p = N.OfParams()
+    if direct_sums:
+        flags |= N.DVC_FLAG_OF_DIRECT_SUMS
     p.width, p.height = int(width), int(height)
     p.flow_threshold = float(flow_threshold)
     p.quant = float(quantization_level)

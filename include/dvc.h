@@ -66,6 +66,9 @@ extern "C" {
                                      NULL (= the legacy default stream);
                                      without the flag NULL means "no caller
                                      stream"                                    */
+#define DVC_FLAG_OF_DIRECT_SUMS 0x10u /* OF: direct per-pixel 9x9 box sums instead
+                                     of OpenCV's running sums (the default,
+                                     FarnebackUpdateFlow_Blur's order)          */
 
 /* ---- frame-differencing (FD) path ------------------------------------------ */
 

@@ -390,9 +390,11 @@ class OfParams(ctypes.Structure):
 
 
 def of_params(width, height, flow_threshold=0.5, alpha_fraction=0.2, window_size=30, morph_kernel=2,
-              quant=100.0) -> OfParams:
-    """motion_compression_opt.py:29-31 kwargs + the hard-coded Farneback arguments (of:72-81)."""
+              quant=100.0, direct_sums=False) -> OfParams:
+    """motion_compression_opt.py:29-31 kwargs + the hard-coded Farneback arguments (of:72-81).
+    ``direct_sums``: direct per-pixel box sums instead of OpenCV's running sums."""
     p = OfParams()
+    p.flags = 0x10 if direct_sums else 0
     p.width, p.height = int(width), int(height)
     p.flow_threshold, p.quant = float(flow_threshold), float(quant)
     p.alpha_fraction, p.window, p.morph_kernel = float(alpha_fraction), int(window_size), int(morph_kernel)
@@ -431,12 +433,16 @@ def _of_lib():
 
 
 def farneback(prev: np.ndarray, nxt: np.ndarray, pyr_scale=0.3, levels=2, winsize=9, iterations=2, poly_n=5,
-              poly_sigma=1.1) -> np.ndarray:
+              poly_sigma=1.1, sliding=True) -> np.ndarray:
     prev, nxt = np.ascontiguousarray(prev, np.uint8), np.ascontiguousarray(nxt, np.uint8)
     H, W = prev.shape
     flow = np.empty((H, W, 2), np.float32)
-    _of_lib().oc_farneback(_u8(prev), _u8(nxt), W, H, pyr_scale, levels, winsize, iterations, poly_n, poly_sigma,
-                           flow.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    set_sliding(sliding)
+    try:
+        _of_lib().oc_farneback(_u8(prev), _u8(nxt), W, H, pyr_scale, levels, winsize, iterations, poly_n,
+                               poly_sigma, flow.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    finally:
+        set_sliding(True)
     return flow
 
 
@@ -455,14 +461,15 @@ def fb_level_poly(gray: np.ndarray, k: int, pyr_scale=0.3, poly_n=5, poly_sigma=
     return R.reshape(-1)[: h.value * w.value * 5].reshape(h.value, w.value, 5).copy()
 
 
-def fb_iteration(R0: np.ndarray, R1: np.ndarray, flow: np.ndarray, winsize=9) -> np.ndarray:
-    """One FarnebackUpdateMatrices + FarnebackUpdateFlow_Blur step (flow_in -> flow_out)."""
+def fb_iteration(R0: np.ndarray, R1: np.ndarray, flow: np.ndarray, winsize=9, sliding=True) -> np.ndarray:
+    """One FarnebackUpdateMatrices + FarnebackUpdateFlow_Blur step (flow_in -> flow_out),
+    box sums in OpenCV's running order (sliding) or direct."""
     h, w = R0.shape[:2]
     R0, R1 = np.ascontiguousarray(R0, np.float32), np.ascontiguousarray(R1, np.float32)
     f = np.ascontiguousarray(flow, np.float32).copy()
     M = np.empty((h, w, 5), np.float32)
     _of_lib().oc_update_matrices(_fp(R0), _fp(R1), _fp(f), w, h, _fp(M), 0, h)
-    _of_lib().oc_update_flow_box(_fp(M), w, h, winsize, _fp(f))
+    (_of_lib().oc_update_flow_box_sliding if sliding else _of_lib().oc_update_flow_box)(_fp(M), w, h, winsize, _fp(f))
     return f
 
 
@@ -490,8 +497,9 @@ def of_compress(bgr: np.ndarray, mask: np.ndarray, quant=100.0) -> np.ndarray:
 
 
 def set_sliding(on: bool) -> None:
-    """Box sums of FarnebackUpdateFlow_Blur: OpenCV's incremental (sliding)
-    accumulation (True) or the direct per-pixel sums the HIP kernels use (False)."""
+    """Box sums of a standalone oc_farneback call: OpenCV's incremental (sliding)
+    accumulation (True, the default) or direct per-pixel sums (False). OracleOF
+    handles choose by their own ``direct_sums`` argument."""
     _of_lib().oc_of_set_sliding(1 if on else 0)
 
 

@@ -17,11 +17,12 @@
  * Farneback follows OpenCV 4.11 optflowgf.cpp (pyramid of blurred + bilinearly
  * resized float images, FarnebackPolyExp, FarnebackUpdateMatrices,
  * FarnebackUpdateFlow_Blur with the box window; flags = 0), restated in plain
- * C. Two deliberate, documented choices: the 9x9 box sums of the update step are
- * direct double-precision sums in a fixed order (OpenCV slides them
- * incrementally), and every float expression is evaluated without contraction
- * (-ffp-contract=off). The HIP kernels use the same order, so the two agree to
- * the last bit; agreement with cv2 itself is "OCV-unverified" (no cv2 here).
+ * C. The 9x9 box sums of the update step follow OpenCV's running sums
+ * (oc_update_flow_box_sliding) unless the handle asks for direct per-pixel
+ * double sums (DVC_FLAG_OF_DIRECT_SUMS, oc_update_flow_box), and every float
+ * expression is evaluated without contraction (-ffp-contract=off). The HIP
+ * kernels implement both orders the same way, so each pair agrees to the last
+ * bit; agreement with cv2 itself is "OCV-unverified" (no cv2 here).
  */
 #include <float.h>
 #include <math.h>
@@ -350,7 +351,7 @@ void oc_update_flow_box_sliding(const float* M, int W, int H, int bs, float* flo
     free(buf);
 }
 
-static int oc_sliding = 0;
+static int oc_sliding = 1;   /* OpenCV's order by default */
 void oc_of_set_sliding(int on) { oc_sliding = on; }
 
 /* Pyramid level geometry of calcOpticalFlowFarneback (min_size 32). */
@@ -597,8 +598,11 @@ int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_
     int W = p->width, H = p->height;
     size_t N = (size_t)W * H;
     oc_bgr2gray(bgr, pitch, W, H, h->gray);                                         /* of:71 */
+    const int saved = oc_sliding;                 /* the handle's box-sum order (DVC_FLAG_OF_DIRECT_SUMS) */
+    oc_sliding = !(p->flags & DVC_FLAG_OF_DIRECT_SUMS);
     oc_farneback(h->prev, h->gray, W, H, p->pyr_scale, p->levels, p->winsize, p->iterations, p->poly_n,
                  p->poly_sigma, h->flow);                                           /* of:72-81 */
+    oc_sliding = saved;
     uint8_t* slot = h->ring[h->head];                                               /* of:84, deque */
     for (size_t i = 0; i < N; ++i) {
         float fx = h->flow[2 * i], fy = h->flow[2 * i + 1];

@@ -21,7 +21,8 @@ def _first_diff(g, r):
 def _run_pair(dvc_amd, oracle, frames, batch=0, **kw):
     """Per-frame (batch=0) or batched GPU run vs the oracle; returns GPU stats."""
     H, W = frames.shape[1:3]
-    okw = {k: v for k, v in kw.items() if k in ("flow_threshold", "alpha_fraction", "window_size", "morph_kernel")}
+    okw = {k: v for k, v in kw.items()
+           if k in ("flow_threshold", "alpha_fraction", "window_size", "morph_kernel", "direct_sums")}
     gpu = dvc_amd.OFWorker(W, H, device=0, keep_planes=True, max_batch=max(batch, 1), **kw)
     ref = oracle.OracleOF(W, H, **okw)
     gpu.prime(frames[0])
@@ -82,7 +83,7 @@ def test_of_stages(gpu_lib, oracle_lib, W, H):
                 raise AssertionError(f"R level {k} ({'prev' if what else 'cur'}): {_first_diff(got, want)}, "
                                      f"max abs {np.abs(got - want).max()}")
     R0, R1 = oracle_lib.fb_level_poly(g0, L), oracle_lib.fb_level_poly(g1, L)
-    f1 = oracle_lib.fb_iteration(R0, R1, np.zeros(R0.shape[:2] + (2,), np.float32))
+    f1 = oracle_lib.fb_iteration(R0, R1, np.zeros(R0.shape[:2] + (2,), np.float32))   # OpenCV's running sums
     got = gpu.debug_read(2, L)
     assert np.array_equal(got.view(np.uint32), f1.view(np.uint32)), f"iteration 0 flow: {_first_diff(got, f1)}"
     want = oracle_lib.farneback(g0, g1)
@@ -103,9 +104,24 @@ def test_of_parity_synthetic(gpu_lib, oracle_lib, W, H, n, seed, noisy):
     _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=seed, noisy=noisy))
 
 
-def test_of_parity_1080p(gpu_lib, oracle_lib):
+@pytest.mark.parametrize("direct", [False, True])
+def test_of_parity_1080p(gpu_lib, oracle_lib, direct):
+    """Both box-sum orders: OpenCV's running sums (k_flow_scan, the default) and
+    direct per-pixel sums (k_flow, DVC_FLAG_OF_DIRECT_SUMS), each vs the oracle
+    computing the same order."""
     from dvc_amd.synthetic import clip
-    _run_pair(gpu_lib, oracle_lib, clip(1920, 1080, 3, seed=3))
+    _run_pair(gpu_lib, oracle_lib, clip(1920, 1080, 3, seed=3), direct_sums=direct)
+
+
+@pytest.mark.parametrize("W,H,kw", [
+    (328, 184, dict(direct_sums=True)),
+    (640, 360, dict(direct_sums=True, window_size=5)),
+    (96, 64, {}),                        # one strip, one pyramid level
+    (136, 72, dict(batch=3)),            # partial last strip, batched
+])
+def test_of_box_orders(gpu_lib, oracle_lib, W, H, kw):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(W, H, 5, seed=W), **kw)
 
 
 def test_of_parity_window_eviction(gpu_lib, oracle_lib):

@@ -3,8 +3,8 @@
 OpenCV's FarnebackUpdateFlow_Blur accumulates the 9x9 box sums incrementally
 (a vertical running double sum per column fed with float row differences, a
 horizontal running double sum per row; oracle/of_oracle.c
-oc_update_flow_box_sliding); the oracle's default and the HIP kernels use
-direct per-pixel double sums. The running sums carry rounding residue along a
+oc_update_flow_box_sliding) — the oracle's and the GPU's default (k_flow_scan);
+DVC_FLAG_OF_DIRECT_SUMS selects direct per-pixel double sums (k_flow). The running sums carry rounding residue along a
 column or row (after a textured region the residue of its large values stays
 in the sum over a flat one), so flow values differ — up to ~0.4 px where G is
 near singular — but the thresholded, voted, morphology-closed rectangle mask
@@ -19,19 +19,15 @@ from tests.golden.cases_of import CASES
 
 
 def _run(oracle, frames, kw, sliding):
-    oracle.set_sliding(sliding)
-    try:
-        H, W = frames.shape[1:3]
-        o = oracle.OracleOF(W, H, **kw)
-        o.prime(frames[0])
-        out = []
-        for f in frames[1:]:
-            mk, cp, fl = o.step(f)
-            out.append((mk, cp, fl, o.plane(0)))
-        o.close()
-        return out
-    finally:
-        oracle.set_sliding(False)
+    H, W = frames.shape[1:3]
+    o = oracle.OracleOF(W, H, direct_sums=not sliding, **kw)
+    o.prime(frames[0])
+    out = []
+    for f in frames[1:]:
+        mk, cp, fl = o.step(f)
+        out.append((mk, cp, fl, o.plane(0)))
+    o.close()
+    return out
 
 
 @pytest.mark.parametrize("name", list(CASES))
