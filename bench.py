@@ -151,6 +151,8 @@ def main():
                          "dvc_host_alloc buffers DMA'd directly, pageable = numpy arrays staged by the library)")
     ap.add_argument("--feeds", type=int, default=1,
                     help="independent feeds per GPU, one handle and one host thread each (config 4's unit)")
+    ap.add_argument("--of-direct", action="store_true",
+                    help="OF: direct per-pixel box sums (DVC_FLAG_OF_DIRECT_SUMS) instead of OpenCV's running sums")
     ap.add_argument("--cpu-cores", type=int, default=1,
                     help="CPU baseline: this many feeds on this many host processes (1 = single core)")
     args = ap.parse_args()
@@ -209,7 +211,7 @@ def main():
 
     def make_worker(f, ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
-        kw = {} if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
+        kw = dict(direct_sums=args.of_direct) if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
                                 release_factor=args.release_factor)
         w = cls(W, H, device=local, device_ptrs=not host_io, ktiming=ktiming, max_batch=batch, **kw)
         w.prime(inputs[f][2])
@@ -295,6 +297,8 @@ def main():
             workload += f"_{args.io}_io"
         if args.per_frame:
             workload += "_per_frame"
+        if of and args.of_direct:
+            workload += "_direct_sums"
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
             workload += f"_b{args.block_size}_k{args.kernel_size}_r{args.release_factor:g}"
         if of:   # kn counts level-0 k_flow launches (iterations per batch)

@@ -39,6 +39,25 @@
 
 namespace dvc {
 
+// R (5 floats a pixel, 20 B: only 4-B aligned) read with dwordx4/x2 loads
+// (unaligned global access is on under ROCm): 2 loads for a pixel's 5
+// channels, 3 for two adjacent pixels' 10, instead of 5 and 10 dword loads —
+// the address rate (TA), not the bytes, bounds the M gathers.
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ void ld5(const float* p, float* o)
+{
+    const f4u a = *reinterpret_cast<const f4u*>(p);
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = p[4];
+}
+__device__ __forceinline__ void ld10(const float* p, float* o)
+{
+    const f4u a = *reinterpret_cast<const f4u*>(p), b = *reinterpret_cast<const f4u*>(p + 4);
+    const f2u c = *reinterpret_cast<const f2u*>(p + 8);
+    o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w, o[8] = c.x,
+    o[9] = c.y;
+}
+
 namespace {
 
 constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
@@ -386,8 +405,7 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
                 dyv[u] = v[1] * g.up;
             }
             const float* r0 = R0 + 5u * pix;
-#pragma unroll
-            for (int c = 0; c < 5; ++c) r0v[u][c] = r0[c];
+            ld5(r0, r0v[u]);
         }
         float pq[MQ][20];
         float fxv[MQ], fyv[MQ];
@@ -402,11 +420,8 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
             const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
             const float* p = R1 + 5u * (uint32_t)(y1c * w + x1c);
             const float* q = p + 5u * (uint32_t)w;
-#pragma unroll
-            for (int c = 0; c < 10; ++c) {
-                pq[u][c] = p[c];
-                pq[u][10 + c] = q[c];
-            }
+            ld10(p, pq[u]);
+            ld10(q, pq[u] + 10);
         }
 #pragma unroll
         for (int u = 0; u < MQ; ++u) {
@@ -621,81 +636,86 @@ struct ScanArgs {
 // SW + 2m + 1 columns x 5 doubles) and its horizontal sums (RB x SW x 5 doubles)
 __host__ __device__ constexpr int scan_ring(int rb, int m) { return rb + 2 * m + 1; }
 __host__ __device__ constexpr int scan_nc(int sw, int m) { return sw + 2 * m + 1; }
+// sG rows padded to sw*5 + 5 doubles (= 5 mod 32): the horizontal chains'
+// lanes (row i, channel c) fall on distinct LDS bank pairs (at most 2-way)
+__host__ __device__ constexpr int scan_gs(int sw) { return sw * 5 + 5; }
 inline size_t scan_lds_bytes(int sw, int rb, int m)
 {
     return (size_t)scan_ring(rb, m) * scan_nc(sw, m) * 5 * 4 + (size_t)rb * scan_nc(sw, m) * 5 * 8 +
-           (size_t)rb * sw * 5 * 8;
+           (size_t)rb * scan_gs(sw) * 8;
 }
 
-// M of FarnebackUpdateMatrices (oc_update_matrices) at MQ positions, each
-// (x, y) inside the level; results to LDS at dst[u] (5 floats). All loads of
-// the MQ positions are issued before any of their arithmetic.
+// M of FarnebackUpdateMatrices (oc_update_matrices) at MQ positions (x, y)
+// inside the level, in three stages so a caller can overlap each stage's
+// loads with other work: (1) the flow loads, (2) the R0 loads and the
+// displaced bilinear R1 loads (their address needs the flow), (3) the
+// arithmetic and the LDS store of the 5 floats at off[u] of the M ring.
 template <int MQ>
-__device__ __forceinline__ void mat_positions(const FlowArgs& A, const float* __restrict__ R0,
-                                              const float* __restrict__ R1, const float* src, const int (&xs)[MQ],
-                                              const int (&ys)[MQ], const bool (&ok)[MQ], float* const (&dst)[MQ])
-{
-    const OfGeom& g = A.g;
-    const int w = A.lv.w, h = A.lv.h;
-    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
-    float dxv[MQ], dyv[MQ], r0v[MQ][5];
-#pragma unroll
-    for (int u = 0; u < MQ; ++u) {
-        const uint32_t pix = (uint32_t)(ys[u] * w + xs[u]);
-        dxv[u] = 0.f;
-        dyv[u] = 0.f;
-        if (A.src_mode == 2) {   // uniform
-            const float2 f = *reinterpret_cast<const float2*>(src + 2u * pix);
-            dxv[u] = f.x;
-            dyv[u] = f.y;
-        } else if (A.src_mode == 1) {
-            const LinTap ty = A.lv.uy[ys[u]], tx = A.lv.ux[xs[u]];
-            const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
-            const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
-            float v[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float t0 = ra[tx.s0 * 2 + c] * tx.w0 + ra[tx.s1 * 2 + c] * tx.w1;
-                const float t1 = rb[tx.s0 * 2 + c] * tx.w0 + rb[tx.s1 * 2 + c] * tx.w1;
-                v[c] = t0 * ty.w0 + t1 * ty.w1;
-            }
-            dxv[u] = v[0] * g.up;
-            dyv[u] = v[1] * g.up;
-        }
-        const float* r0 = R0 + 5u * pix;
-#pragma unroll
-        for (int c = 0; c < 5; ++c) r0v[u][c] = r0[c];
-    }
-    float pq[MQ][20], fxv[MQ], fyv[MQ];
+struct MatPos {
+    int xs[MQ], ys[MQ], off[MQ];
+    bool ok[MQ];
+    float dx[MQ], dy[MQ], r0[MQ][5];   // stage 1
+    float fx[MQ], fy[MQ], pq[MQ][20];  // stage 2
     bool inb[MQ];
+};
+
+// stage 1: the flow loads (src_mode 2; the scan kernel's source flow is never
+// the coarser level's: k_flow_up upsamples it to a flow buffer first)
+template <int MQ, int SMODE>
+__device__ __forceinline__ void mat_stage1(const FlowArgs& A, const float* src, MatPos<MQ>& P)
+{
+    const int w = A.lv.w;
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
-        float fx = (float)xs[u] + dxv[u], fy = (float)ys[u] + dyv[u];
+        const uint32_t pix = (uint32_t)(P.ys[u] * w + P.xs[u]);
+        P.dx[u] = 0.f;
+        P.dy[u] = 0.f;
+        if constexpr (SMODE == 2) {
+            const float2 f = *reinterpret_cast<const float2*>(src + 2u * pix);
+            P.dx[u] = f.x;
+            P.dy[u] = f.y;
+        }
+    }
+}
+
+template <int MQ>
+__device__ __forceinline__ void mat_stage2(const FlowArgs& A, const float* __restrict__ R0,
+                                           const float* __restrict__ R1, MatPos<MQ>& P)
+{
+    const int w = A.lv.w, h = A.lv.h;
+#pragma unroll
+    for (int u = 0; u < MQ; ++u) {
+        ld5(R0 + 5u * (uint32_t)(P.ys[u] * w + P.xs[u]), P.r0[u]);   // (independent of the flow)
+        const float fx = (float)P.xs[u] + P.dx[u], fy = (float)P.ys[u] + P.dy[u];
         const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
-        fxv[u] = fx - (float)x1;
-        fyv[u] = fy - (float)y1;
-        inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
+        P.fx[u] = fx - (float)x1;
+        P.fy[u] = fy - (float)y1;
+        P.inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
         const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
         const float* p = R1 + 5u * (uint32_t)(y1c * w + x1c);
         const float* q = p + 5u * (uint32_t)w;
-#pragma unroll
-        for (int c = 0; c < 10; ++c) {
-            pq[u][c] = p[c];
-            pq[u][10 + c] = q[c];
-        }
+        ld10(p, P.pq[u]);
+        ld10(q, P.pq[u] + 10);
     }
+}
+
+template <int MQ>
+__device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& P, float* sM)
+{
+    const int w = A.lv.w, h = A.lv.h;
+    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
-        if (!ok[u]) continue;
-        const int x = xs[u], y = ys[u];
-        const float dx = dxv[u], dy = dyv[u], fx = fxv[u], fy = fyv[u];
-        const float* r0 = r0v[u];
-        const float* p = pq[u];
-        const float* q = pq[u] + 10;
+        if (!P.ok[u]) continue;
+        const int x = P.xs[u], y = P.ys[u];
+        const float dx = P.dx[u], dy = P.dy[u], fx = P.fx[u], fy = P.fy[u];
+        const float* r0 = P.r0[u];
+        const float* p = P.pq[u];
+        const float* q = P.pq[u] + 10;
         f32x2 R23, R45;
         float r6;
         const f32x2 R0_01 = {r0[0], r0[1]}, R0_23 = {r0[2], r0[3]};
-        if (inb[u]) {
+        if (P.inb[u]) {
             const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
             const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
             const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
@@ -719,7 +739,7 @@ __device__ __forceinline__ void mat_positions(const FlowArgs& A, const float* __
             R45 = R45 * (f32x2)scale;
             r6 *= scale;
         }
-        float* M = dst[u];
+        float* M = sM + P.off[u];
         const f32x2 G = R45 * R45 + (f32x2)(r6 * r6);
         const f32x2 Hh = (f32x2){R45.x, r6} * (f32x2)R23.x + (f32x2){r6, R45.y} * (f32x2)R23.y;
         M[0] = G.x;
@@ -751,14 +771,16 @@ __device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long
     return true;
 }
 
-template <int SW, int RB>
+template <int SW, int RB, int NT, int SMODE>   // SMODE: 0 zero flow, 2 flow buffer
 __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, double* sG, int* s_alive)
 {
+    static_assert(RB * 5 <= 64, "the horizontal chains of a block fit one wave");
     const FlowArgs& A = S.f;
     const OfGeom& g = A.g;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int w = A.lv.w, h = A.lv.h, m = g.m;
     const int RING = scan_ring(RB, m), NC = scan_nc(SW, m);
+    constexpr int GS = scan_gs(SW);
     const int X0 = s * SW, X1 = min(X0 + SW, w), CX0 = X0 - m - 1, nx = X1 - X0;
     const size_t lvpx = (size_t)w * h;
     const long long a = A.a0 + t;
@@ -771,110 +793,169 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     double* gp_mine = S.gpub + ((size_t)t * S.S + s) * (size_t)h * 5;
     const double* gp_left = s > 0 ? gp_mine - (size_t)h * 5 : nullptr;
     const unsigned long long ep = (unsigned long long)S.epoch << 32;
-    // vertical chains of this thread: (column, channel) ch = tid + 256 k
+    // M positions of rows [rlo, rhi] x the strip's NC columns, ring offsets;
+    // the pipelined blocks' M is done by waves 1.. only (NP threads): wave 0
+    // runs the horizontal chains and the hand-off, whose loads and drain must
+    // not queue behind prefetches (vmcnt is in order)
+    constexpr int NP = NT - 64;
+    constexpr int MQ = (RB * scan_nc(SW, OF_MAX_BOX_M) + NP - 1) / NP;
+    auto place = [&](MatPos<MQ>& P, int q0, int rlo, int npos, int stride) {
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            const int idx = q0 + stride * u;
+            P.ok[u] = idx < npos;
+            const int ii = P.ok[u] ? idx : 0;
+            const int r = rlo + ii / NC, j = ii - (ii / NC) * NC;
+            P.xs[u] = min(max(CX0 + j, 0), w - 1);
+            P.ys[u] = r;
+            P.off[u] = ((r % RING) * NC + j) * 5;
+        }
+    };
+    // the new M rows of the block at y0: rows 0..RB-1+m for the first (vsum's
+    // start needs rows 0..m-1), then y0+m .. y0+RB-1+m, clipped to the level
+    auto block_rows = [&](int y0, int& rlo, int& npos) {
+        rlo = y0 == 0 ? 0 : (y0 + m <= h - 1 ? y0 + m : h);
+        const int rhi = min(y0 + RB - 1 + m, h - 1);
+        npos = rhi >= rlo ? (rhi - rlo + 1) * NC : 0;
+    };
+    // vertical chains of this thread: (column, channel) ch = tid + NT k
     const int nch = NC * 5;
-    constexpr int KV = (scan_nc(SW, OF_MAX_BOX_M) * 5 + 255) / 256;
+    constexpr int KV = (scan_nc(SW, OF_MAX_BOX_M) * 5 + NT - 1) / NT;
     double vsum[KV];
 #pragma unroll
     for (int k = 0; k < KV; ++k) vsum[k] = 0.0;
     auto mrow = [&](int r) { return sM + (size_t)(r % RING) * NC * 5; };
-    for (int y0 = 0; y0 < h; y0 += RB) {
-        const int yb = y0 / RB, nrow = min(RB, h - y0);
-        // 1. M rows [rlo, rhi] (block 0 also rows 0..m-1 for the start)
-        const int rlo = y0 == 0 ? 0 : (y0 + m <= h - 1 ? y0 + m : h);
-        const int rhi = min(y0 + RB - 1 + m, h - 1);
-        const int npos = rhi >= rlo ? (rhi - rlo + 1) * NC : 0;
-        constexpr int MQ = 3;
-        for (int q0 = tid; q0 < npos; q0 += 256 * MQ) {
-            int xs[MQ], ys[MQ];
-            bool ok[MQ];
-            float* d[MQ];
-#pragma unroll
-            for (int u = 0; u < MQ; ++u) {
-                const int idx = q0 + 256 * u;
-                ok[u] = idx < npos;
-                const int ii = ok[u] ? idx : 0;
-                const int r = rlo + ii / NC, j = ii - (ii / NC) * NC;
-                xs[u] = min(max(CX0 + j, 0), w - 1);
-                ys[u] = r;
-                d[u] = mrow(r) + j * 5;
-            }
-            mat_positions<MQ>(A, R0, R1, src, xs, ys, ok, d);
+    {   // 1. M of the first block, unpipelined
+        int rlo, npos;
+        block_rows(0, rlo, npos);
+        for (int q0 = tid; q0 < npos; q0 += NT * MQ) {
+            MatPos<MQ> P;
+            place(P, q0, rlo, npos, NT);
+            mat_stage1<MQ, SMODE>(A, src, P);
+            mat_stage2<MQ>(A, R0, R1, P);
+            mat_stage3<MQ>(A, P, sM);
         }
         __syncthreads();
+    }
+    MatPos<MQ> P;   // the next block's M positions, in flight across the block's phases
+    int prow[MQ], pcol[MQ], pidx[MQ];   // this thread's pipelined positions: row in block, column
+#pragma unroll
+    for (int u = 0; u < MQ; ++u) {
+        pidx[u] = tid - 64 + NP * u;
+        prow[u] = max(pidx[u], 0) / NC;
+        pcol[u] = max(pidx[u], 0) - prow[u] * NC;
+    }
+    for (int y0 = 0; y0 < h; y0 += RB) {
+        const int yb = y0 / RB, nrow = min(RB, h - y0);
+        int nlo, nnpos;
+        block_rows(y0 + RB, nlo, nnpos);
+        const bool pipe = nnpos > 0 && tid >= 64;   // wave-uniform; nnpos <= RB * NC <= NP * MQ
+        if (pipe) {                                 // 1'. the next block's flow and R0 loads
+            const int slo = nlo % RING;
+#pragma unroll
+            for (int u = 0; u < MQ; ++u) {
+                P.ok[u] = pidx[u] < nnpos;
+                const int r = P.ok[u] ? nlo + prow[u] : nlo, sl = slo + (P.ok[u] ? prow[u] : 0);
+                P.xs[u] = min(max(CX0 + pcol[u], 0), w - 1);
+                P.ys[u] = r;
+                P.off[u] = ((sl >= RING ? sl - RING : sl) * NC + pcol[u]) * 5;
+            }
+            mat_stage1<MQ, SMODE>(A, src, P);
+        }
         // 2. vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ch = tid + 256 * k;
+            const int ch = tid + NT * k;
             if (ch >= nch) continue;
             const int j = ch / 5, c = ch - 5 * j;
             if (y0 == 0) {   // vsum = row0 * (m+2) (a float product) + rows 1..m-1
                 vsum[k] = (double)(mrow(0)[j * 5 + c] * (float)(m + 2));
                 for (int r = 1; r < m; ++r) vsum[k] += (double)mrow(min(r, h - 1))[j * 5 + c];
             }
+            // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0), stepped
+            const int slot_last = (h - 1) % RING;
+            int sa = (y0 + m) % RING, sb = y0 - m - 1 >= 0 ? (y0 - m - 1) % RING : 0;
             for (int i = 0; i < nrow; ++i) {
                 const int y = y0 + i;
-                const float dd = mrow(min(y + m, h - 1))[j * 5 + c] - mrow(max(y - m - 1, 0))[j * 5 + c];
+                const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
+                const float dd = sM[(ta * NC + j) * 5 + c] - sM[(tb * NC + j) * 5 + c];
                 vsum[k] += (double)dd;
-                sV[((size_t)i * NC + j) * 5 + c] = vsum[k];
+                sV[(i * NC + j) * 5 + c] = vsum[k];
+                sa = sa + 1 == RING ? 0 : sa + 1;
+                if (y - m - 1 >= 0) sb = sb + 1 == RING ? 0 : sb + 1;
             }
         }
-        __syncthreads();
-        // 3a. the horizontal increments vsum[x+m] - vsum[x-m-1] (independent: all
-        // threads) into sG; meanwhile thread 0 waits for the left strip's block
+        __syncthreads();   // the M ring is free from here: no reader until the next block's step 2
+        // 3a. the horizontal increments vsum[x+m] - vsum[x-m-1] (independent:
+        // all threads) into sG; meanwhile thread 0 waits for the left strip's block
         if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
-        for (int e = tid; e < nrow * SW * 5; e += 256) {
+        for (int e = tid; e < nrow * SW * 5; e += NT) {
             const int i = e / (SW * 5), rem = e - i * (SW * 5), xl = rem / 5, c = rem - 5 * xl;
             if (xl >= nx) continue;
             const double* v = sV + (size_t)i * NC * 5 + c;
             const int x = X0 + xl;
-            sG[e] = v[(x + m - CX0) * 5] - v[(x - m - 1 - CX0) * 5];
+            sG[i * GS + rem] = v[(x + m - CX0) * 5] - v[(x - m - 1 - CX0) * 5];
         }
         __syncthreads();
-        // 3b. the running sums, lanes (row i, channel c); loads batched ahead of
-        // the dependent adds; the state after the last column goes to the right
-        if (tid < nrow * 5) {
-            const int i = tid / 5, c = tid - 5 * i;
-            const double* v = sV + (size_t)i * NC * 5 + c;
-            double acc;
-            if (s == 0) {
-                acc = v[(0 - CX0) * 5] * (double)(m + 2);
-                for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
-            } else {
-                acc = __hip_atomic_load(gp_left + (size_t)(y0 + i) * 5 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            double* gr = sG + (size_t)i * SW * 5 + c;
-            constexpr int U = 8;
-            int xl = 0;
-            for (; xl + U <= nx; xl += U) {
-                double dv[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) dv[u] = gr[(xl + u) * 5];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    acc += dv[u];
-                    gr[(xl + u) * 5] = acc;
+        // 3b. the running sums, wave 0 lanes (row i, channel c); loads batched
+        // ahead of the dependent adds. The state after the last column goes to
+        // the right neighbour: payload, drain (vmcnt: one wave), flag.
+        if (tid < 64) {
+            if (tid < nrow * 5) {
+                const int i = tid / 5, c = tid - 5 * i;
+                const double* v = sV + (size_t)i * NC * 5 + c;
+                double acc;
+                if (s == 0) {
+                    acc = v[(0 - CX0) * 5] * (double)(m + 2);
+                    for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
+                } else {
+                    acc = __hip_atomic_load(gp_left + (size_t)(y0 + i) * 5 + c, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
+                double* gr = sG + i * GS + c;
+                constexpr int U = 8;
+                int xl = 0;
+                for (; xl + U <= nx; xl += U) {
+                    double dv[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) dv[u] = gr[(xl + u) * 5];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        acc += dv[u];
+                        gr[(xl + u) * 5] = acc;
+                    }
+                }
+                for (; xl < nx; ++xl) {
+                    acc += gr[xl * 5];
+                    gr[xl * 5] = acc;
+                }
+                if (s + 1 < S.S)
+                    __hip_atomic_store(gp_mine + (size_t)(y0 + i) * 5 + c, acc, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             }
-            for (; xl < nx; ++xl) {
-                acc += gr[xl * 5];
-                gr[xl * 5] = acc;
+            if (s + 1 < S.S) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's payload stores have landed
+                if (tid == 0)
+                    __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (s + 1 < S.S)
-                __hip_atomic_store(gp_mine + (size_t)(y0 + i) * 5 + c, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (s + 1 < S.S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the payload stores have landed
+        }
+        // 1''. waves 1..: the next block's displaced R1 loads and M into the
+        // ring, alongside wave 0's chains (the ring has no reader until step 2)
+        if (pipe) {
+            mat_stage2<MQ>(A, R0, R1, P);
+            mat_stage3<MQ>(A, P, sM);
         }
         __syncthreads();
-        if (s + 1 < S.S && tid == 0)
-            __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool alive = *s_alive;   // uniform: written before the previous barrier
         // 4. flow = G^-1 h per pixel of the block (a wave = 64 / SW rows of SW columns)
-        for (int e = tid; e < RB * SW; e += 256) {
+        for (int e = tid; e < RB * SW; e += NT) {
             const int i = e / SW, xl = e - i * SW;
             const int y = y0 + i, x = X0 + xl;
             const bool act = i < nrow && xl < nx;
             float fxo = 0.f, fyo = 0.f;
             if (act) {
-                const double* gg = sG + (size_t)(i * SW + xl) * 5;
+                const double* gg = sG + i * GS + xl * 5;
                 const double g11 = gg[0] * g.box_scale, g12 = gg[1] * g.box_scale, g22 = gg[2] * g.box_scale;
                 const double h1 = gg[3] * g.box_scale, h2 = gg[4] * g.box_scale;
                 const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
@@ -901,20 +982,20 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
             }
         }
-        __syncthreads();
-        if (!*s_alive) break;   // uniform (read after the barrier): an aborted launch drains
+        // no barrier: the next block writes sV (unread here) before its first
+        // barrier and sG only after it
+        if (!alive) break;   // an aborted launch drains
     }
-    (void)wave;
 }
 
-template <int SW, int RB>
-__global__ void __launch_bounds__(256) k_flow_scan(ScanArgs S)
+template <int SW, int RB, int NT, int SMODE>
+__global__ void __launch_bounds__(NT, NT == 512 ? 4 : 2) k_flow_scan(ScanArgs S)
 {
     extern __shared__ __attribute__((aligned(16))) double lds_s[];
     const int m = S.f.g.m;
     double* sV = lds_s;
     double* sG = sV + (size_t)RB * scan_nc(SW, m) * 5;
-    float* sM = reinterpret_cast<float*>(sG + (size_t)RB * SW * 5);
+    float* sM = reinterpret_cast<float*>(sG + (size_t)RB * scan_gs(SW));
     __shared__ int item, alive;
     const int total = S.S * S.f.n;
     for (;;) {
@@ -926,7 +1007,7 @@ __global__ void __launch_bounds__(256) k_flow_scan(ScanArgs S)
         const int it = item;
         __syncthreads();
         if (it >= total) break;
-        scan_strip<SW, RB>(S, it / S.S, it % S.S, sM, sV, sG, &alive);
+        scan_strip<SW, RB, NT, SMODE>(S, it / S.S, it % S.S, sM, sV, sG, &alive);
     }
 }
 
@@ -1379,6 +1460,29 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
     return hipGetLastError();
 }
 
+// The coarser level's final flow bilinearly upsampled (the taps ux/uy of
+// the level, x g.up) into a flow buffer of this level: the value the direct
+// kernel computes inline per position (src_mode 1), same products, same order.
+__global__ void __launch_bounds__(256) k_flow_up(FlowArgs A, float* __restrict__ out)
+{
+    const int w = A.lv.w, h = A.lv.h;
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, t = blockIdx.z;
+    if (x >= w || y >= h) return;
+    const float* src = A.src + (size_t)t * A.sw * A.sh * 2;
+    const LinTap ty = A.lv.uy[y], tx = A.lv.ux[x];
+    const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
+    const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
+    float v[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const float t0 = ra[tx.s0 * 2 + c] * tx.w0 + ra[tx.s1 * 2 + c] * tx.w1;
+        const float t1 = rb[tx.s0 * 2 + c] * tx.w0 + rb[tx.s1 * 2 + c] * tx.w1;
+        v[c] = t0 * ty.w0 + t1 * ty.w1;
+    }
+    *reinterpret_cast<float2*>(out + ((size_t)t * w * h + (size_t)y * w + x) * 2) =
+        make_float2(v[0] * A.g.up, v[1] * A.g.up);
+}
+
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
                           hipStream_t s, unsigned int* epoch)
 {
@@ -1416,13 +1520,12 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
             if (g.sliding) {   // OpenCV's running box sums: strip wavefront
-                // strip width x rows per block: 64 x 8 (measured best of 32/64 x 8/16 at 1080p;
-                // DVC_OF_SCAN = "32x8", "32x16", "64x16" for sweeps)
+                // strips of 64 columns x blocks of 8 rows, 512 threads (DVC_OF_SCAN=64x8x256: 256 threads)
                 static const int scan_cfg = [] {
                     const char* e = getenv("DVC_OF_SCAN");
-                    return !e ? 1 : !strcmp(e, "32x8") ? 0 : !strcmp(e, "32x16") ? 2 : !strcmp(e, "64x16") ? 3 : 1;
+                    return e && !strcmp(e, "64x8x256") ? 1 : 0;
                 }();
-                const int sw = scan_cfg & 1 ? 64 : 32, rb = scan_cfg & 2 ? 16 : 8;
+                const int sw = 64, rb = 8;
                 ScanArgs S{};
                 S.f = A;
                 S.S = (L.w + sw - 1) / sw;
@@ -1431,15 +1534,27 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 S.next = b.scan_ctr;
                 S.abort = b.scan_abort;
                 S.epoch = ++*epoch;
+                if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
+                    // until iteration 1 writes it), then read it as a flow buffer
+                    float* up = L.flow[1];
+                    hipLaunchKernelGGL(k_flow_up, dim3((L.w + 255) / 256, L.h, n), dim3(256), 0, s, A, up);
+                    S.f.src_mode = 2;
+                    S.f.src = up;
+                }
                 hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4, s);
                 if (e != hipSuccess) return e;
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
                 const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
-                if (scan_cfg == 0) hipLaunchKernelGGL((k_flow_scan<32, 8>), dim3(grid_s), dim3(256), lds_b, s, S);
-                else if (scan_cfg == 1) hipLaunchKernelGGL((k_flow_scan<64, 8>), dim3(grid_s), dim3(256), lds_b, s, S);
-                else if (scan_cfg == 2) hipLaunchKernelGGL((k_flow_scan<32, 16>), dim3(grid_s), dim3(256), lds_b, s, S);
-                else hipLaunchKernelGGL((k_flow_scan<64, 16>), dim3(grid_s), dim3(256), lds_b, s, S);
+                switch (scan_cfg * 2 + (S.f.src_mode == 2)) {
+#define DVC_SCAN_CASE(i, NTv, SM) \
+    case i: hipLaunchKernelGGL((k_flow_scan<64, 8, NTv, SM>), dim3(grid_s), dim3(NTv), lds_b, s, S); break;
+                    DVC_SCAN_CASE(0, 512, 0)
+                    DVC_SCAN_CASE(1, 512, 2)
+                    DVC_SCAN_CASE(2, 256, 0)
+                    DVC_SCAN_CASE(3, 256, 2)
+#undef DVC_SCAN_CASE
+                }
             } else if (g.m == 4) {
                 hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
             } else {
