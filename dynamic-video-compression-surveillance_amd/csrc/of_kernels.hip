@@ -632,17 +632,17 @@ struct ScanArgs {
 };
 
 // strip width SW (columns) and rows per block RB; LDS: the M ring (RB + 2m + 1
-// rows of SW + 2m + 1 columns x 5 floats), the block's vertical sums (RB rows x
-// SW + 2m + 1 columns x 5 doubles) and its horizontal sums (RB x SW x 5 doubles)
+// rows of SW + 2m + 1 columns x 5 floats) and the block's vertical sums (RB
+// rows of SW + 2m + 1 columns x 5 doubles, rows padded to 5 mod 32 doubles so
+// the horizontal chains' lanes (row i, channel c) fall on distinct LDS bank
+// pairs, at most 2-way); the chains overwrite the consumed vertical sums with
+// the horizontal ones in place
 __host__ __device__ constexpr int scan_ring(int rb, int m) { return rb + 2 * m + 1; }
 __host__ __device__ constexpr int scan_nc(int sw, int m) { return sw + 2 * m + 1; }
-// sG rows padded to sw*5 + 5 doubles (= 5 mod 32): the horizontal chains'
-// lanes (row i, channel c) fall on distinct LDS bank pairs (at most 2-way)
-__host__ __device__ constexpr int scan_gs(int sw) { return sw * 5 + 5; }
+__host__ __device__ constexpr int scan_vs(int sw, int m) { return scan_nc(sw, m) * 5 + ((5 - scan_nc(sw, m) * 5) % 32 + 32) % 32; }
 inline size_t scan_lds_bytes(int sw, int rb, int m)
 {
-    return (size_t)scan_ring(rb, m) * scan_nc(sw, m) * 5 * 4 + (size_t)rb * scan_nc(sw, m) * 5 * 8 +
-           (size_t)rb * scan_gs(sw) * 8;
+    return (size_t)scan_ring(rb, m) * scan_nc(sw, m) * 5 * 4 + (size_t)rb * scan_vs(sw, m) * 8;
 }
 
 // M of FarnebackUpdateMatrices (oc_update_matrices) at MQ positions (x, y)
@@ -771,22 +771,23 @@ __device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long
     return true;
 }
 
-template <int SW, int RB, int NT, int SMODE>   // SMODE: 0 zero flow, 2 flow buffer
-__device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, double* sG, int* s_alive)
+// SMODE: 0 zero flow, 2 a flow buffer; MM: the largest box radius m served
+// (sizes the per-thread M positions)
+template <int SW, int RB, int NT, int SMODE, int MM>
+__device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, int* s_alive)
 {
     static_assert(RB * 5 <= 64, "the horizontal chains of a block fit one wave");
     const FlowArgs& A = S.f;
     const OfGeom& g = A.g;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = A.lv.w, h = A.lv.h, m = g.m;
-    const int RING = scan_ring(RB, m), NC = scan_nc(SW, m);
-    constexpr int GS = scan_gs(SW);
+    const int RING = scan_ring(RB, m), NC = scan_nc(SW, m), VS = scan_vs(SW, m);
     const int X0 = s * SW, X1 = min(X0 + SW, w), CX0 = X0 - m - 1, nx = X1 - X0;
     const size_t lvpx = (size_t)w * h;
     const long long a = A.a0 + t;
     const float* __restrict__ R0 = A.lv.R + (size_t)ring(a - 1, g.RS) * lvpx * 5;
     const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
-    const float* src = A.src ? A.src + (size_t)t * (A.src_mode == 1 ? (size_t)A.sw * A.sh : lvpx) * 2 : nullptr;
+    const float* src = SMODE == 2 ? A.src + (size_t)t * lvpx * 2 : nullptr;
     float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
     unsigned long long* myflag = S.flags + (size_t)t * S.S + s;
     const unsigned long long* lflag = s > 0 ? myflag - 1 : nullptr;
@@ -798,7 +799,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     // runs the horizontal chains and the hand-off, whose loads and drain must
     // not queue behind prefetches (vmcnt is in order)
     constexpr int NP = NT - 64;
-    constexpr int MQ = (RB * scan_nc(SW, OF_MAX_BOX_M) + NP - 1) / NP;
+    constexpr int MQ = (RB * scan_nc(SW, MM) + NP - 1) / NP;
     auto place = [&](MatPos<MQ>& P, int q0, int rlo, int npos, int stride) {
 #pragma unroll
         for (int u = 0; u < MQ; ++u) {
@@ -820,11 +821,10 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     };
     // vertical chains of this thread: (column, channel) ch = tid + NT k
     const int nch = NC * 5;
-    constexpr int KV = (scan_nc(SW, OF_MAX_BOX_M) * 5 + NT - 1) / NT;
+    constexpr int KV = (scan_nc(SW, MM) * 5 + NT - 1) / NT;
     double vsum[KV];
 #pragma unroll
     for (int k = 0; k < KV; ++k) vsum[k] = 0.0;
-    auto mrow = [&](int r) { return sM + (size_t)(r % RING) * NC * 5; };
     {   // 1. M of the first block, unpipelined
         int rlo, npos;
         block_rows(0, rlo, npos);
@@ -845,12 +845,13 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         prow[u] = max(pidx[u], 0) / NC;
         pcol[u] = max(pidx[u], 0) - prow[u] * NC;
     }
+    const int slot_last = (h - 1) % RING;
     for (int y0 = 0; y0 < h; y0 += RB) {
         const int yb = y0 / RB, nrow = min(RB, h - y0);
         int nlo, nnpos;
         block_rows(y0 + RB, nlo, nnpos);
         const bool pipe = nnpos > 0 && tid >= 64;   // wave-uniform; nnpos <= RB * NC <= NP * MQ
-        if (pipe) {                                 // 1'. the next block's flow and R0 loads
+        if (pipe) {                                 // 1'. the next block's flow loads
             const int slo = nlo % RING;
 #pragma unroll
             for (int u = 0; u < MQ; ++u) {
@@ -869,41 +870,33 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             if (ch >= nch) continue;
             const int j = ch / 5, c = ch - 5 * j;
             if (y0 == 0) {   // vsum = row0 * (m+2) (a float product) + rows 1..m-1
-                vsum[k] = (double)(mrow(0)[j * 5 + c] * (float)(m + 2));
-                for (int r = 1; r < m; ++r) vsum[k] += (double)mrow(min(r, h - 1))[j * 5 + c];
+                vsum[k] = (double)(sM[j * 5 + c] * (float)(m + 2));
+                for (int r = 1; r < m; ++r) vsum[k] += (double)sM[((min(r, h - 1) % RING) * NC + j) * 5 + c];
             }
             // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0), stepped
-            const int slot_last = (h - 1) % RING;
             int sa = (y0 + m) % RING, sb = y0 - m - 1 >= 0 ? (y0 - m - 1) % RING : 0;
             for (int i = 0; i < nrow; ++i) {
                 const int y = y0 + i;
                 const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
                 const float dd = sM[(ta * NC + j) * 5 + c] - sM[(tb * NC + j) * 5 + c];
                 vsum[k] += (double)dd;
-                sV[(i * NC + j) * 5 + c] = vsum[k];
+                sV[i * VS + ch] = vsum[k];
                 sa = sa + 1 == RING ? 0 : sa + 1;
                 if (y - m - 1 >= 0) sb = sb + 1 == RING ? 0 : sb + 1;
             }
         }
         __syncthreads();   // the M ring is free from here: no reader until the next block's step 2
-        // 3a. the horizontal increments vsum[x+m] - vsum[x-m-1] (independent:
-        // all threads) into sG; meanwhile thread 0 waits for the left strip's block
-        if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
-        for (int e = tid; e < nrow * SW * 5; e += NT) {
-            const int i = e / (SW * 5), rem = e - i * (SW * 5), xl = rem / 5, c = rem - 5 * xl;
-            if (xl >= nx) continue;
-            const double* v = sV + (size_t)i * NC * 5 + c;
-            const int x = X0 + xl;
-            sG[i * GS + rem] = v[(x + m - CX0) * 5] - v[(x - m - 1 - CX0) * 5];
-        }
-        __syncthreads();
-        // 3b. the running sums, wave 0 lanes (row i, channel c); loads batched
-        // ahead of the dependent adds. The state after the last column goes to
-        // the right neighbour: payload, drain (vmcnt: one wave), flag.
         if (tid < 64) {
+            // 3. wave 0: the horizontal recurrence, lanes (row i, channel c):
+            // g += vsum[x+m] - vsum[x-m-1], from the left strip's published
+            // state (strip 0: OpenCV's (m+2) vsum[0] + vsum[1..m-1] start);
+            // g[x] overwrites the consumed vsum[x-m-1] (column x - X0 of sV).
+            // The state after the last column goes to the right neighbour:
+            // payload, drain (vmcnt: one wave), flag.
+            if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
             if (tid < nrow * 5) {
                 const int i = tid / 5, c = tid - 5 * i;
-                const double* v = sV + (size_t)i * NC * 5 + c;
+                double* v = sV + i * VS + c;   // column j at v[5 j]
                 double acc;
                 if (s == 0) {
                     acc = v[(0 - CX0) * 5] * (double)(m + 2);
@@ -912,22 +905,26 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     acc = __hip_atomic_load(gp_left + (size_t)(y0 + i) * 5 + c, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
                 }
-                double* gr = sG + i * GS + c;
+                const int ahead = 2 * m + 1;   // column of vsum[x+m] relative to vsum[x-m-1]
                 constexpr int U = 8;
                 int xl = 0;
-                for (; xl + U <= nx; xl += U) {
-                    double dv[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) dv[u] = gr[(xl + u) * 5];
+                for (; xl + U <= nx; xl += U) {   // all loads of 8 steps before their adds
+                    double da[U], db[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        acc += dv[u];
-                        gr[(xl + u) * 5] = acc;
+                        da[u] = v[(xl + u + ahead) * 5];
+                        db[u] = v[(xl + u) * 5];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        acc += da[u] - db[u];
+                        v[(xl + u) * 5] = acc;
                     }
                 }
                 for (; xl < nx; ++xl) {
-                    acc += gr[xl * 5];
-                    gr[xl * 5] = acc;
+                    const double d = v[(xl + ahead) * 5] - v[xl * 5];
+                    acc += d;
+                    v[xl * 5] = acc;
                 }
                 if (s + 1 < S.S)
                     __hip_atomic_store(gp_mine + (size_t)(y0 + i) * 5 + c, acc, __ATOMIC_RELAXED,
@@ -939,23 +936,22 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-        }
-        // 1''. waves 1..: the next block's displaced R1 loads and M into the
-        // ring, alongside wave 0's chains (the ring has no reader until step 2)
-        if (pipe) {
+        } else if (pipe) {
+            // 1''. waves 1..: the next block's R0 and displaced R1 loads and M
+            // into the ring, alongside wave 0's chains
             mat_stage2<MQ>(A, R0, R1, P);
             mat_stage3<MQ>(A, P, sM);
         }
         __syncthreads();
         const bool alive = *s_alive;   // uniform: written before the previous barrier
-        // 4. flow = G^-1 h per pixel of the block (a wave = 64 / SW rows of SW columns)
+        // 4. flow = G^-1 h per pixel of the block (a wave = one row of 64 columns)
         for (int e = tid; e < RB * SW; e += NT) {
             const int i = e / SW, xl = e - i * SW;
             const int y = y0 + i, x = X0 + xl;
             const bool act = i < nrow && xl < nx;
             float fxo = 0.f, fyo = 0.f;
             if (act) {
-                const double* gg = sG + i * GS + xl * 5;
+                const double* gg = sV + i * VS + xl * 5;
                 const double g11 = gg[0] * g.box_scale, g12 = gg[1] * g.box_scale, g22 = gg[2] * g.box_scale;
                 const double h1 = gg[3] * g.box_scale, h2 = gg[4] * g.box_scale;
                 const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
@@ -968,34 +964,24 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                 const float mag = sqrtf(fxo * fxo + fyo * fyo);   // of:82-83
                 const unsigned long long word = __ballot(act && mag > g.flow_thr);
                 uint64_t* mr = A.mring + (size_t)ring(a, g.RB) * h * g.WW;
-                if constexpr (SW == 64) {
-                    if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
-                } else {   // SW = 32: lanes 0-31 row i, 32-63 row i+1, each half a mask word
-                    uint32_t* mr32 = reinterpret_cast<uint32_t*>(mr);
-                    const int half = (X0 >> 5) & 1;
-                    if ((lane & 31) == 0 && i < nrow) {
-                        mr32[((size_t)y * g.WW + (X0 >> 6)) * 2 + half] = (uint32_t)(word >> (lane & 32));
-                        if (half == 0 && X0 + 32 >= w) mr32[((size_t)y * g.WW + (X0 >> 6)) * 2 + 1] = 0u;
-                    }
-                }
+                if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
                 if (A.dbg_flow && t == A.n - 1 && act)
                     *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
             }
         }
-        // no barrier: the next block writes sV (unread here) before its first
-        // barrier and sG only after it
+        __syncthreads();   // the next block's step 2 overwrites sV
         if (!alive) break;   // an aborted launch drains
     }
 }
 
-template <int SW, int RB, int NT, int SMODE>
+template <int SW, int RB, int NT, int SMODE, int MM>
 __global__ void __launch_bounds__(NT, NT == 512 ? 4 : 2) k_flow_scan(ScanArgs S)
 {
+    static_assert(SW == 64, "a wave's mask ballot is one 64-column mask word");
     extern __shared__ __attribute__((aligned(16))) double lds_s[];
     const int m = S.f.g.m;
     double* sV = lds_s;
-    double* sG = sV + (size_t)RB * scan_nc(SW, m) * 5;
-    float* sM = reinterpret_cast<float*>(sG + (size_t)RB * scan_gs(SW));
+    float* sM = reinterpret_cast<float*>(sV + (size_t)RB * scan_vs(SW, m));
     __shared__ int item, alive;
     const int total = S.S * S.f.n;
     for (;;) {
@@ -1007,7 +993,7 @@ __global__ void __launch_bounds__(NT, NT == 512 ? 4 : 2) k_flow_scan(ScanArgs S)
         const int it = item;
         __syncthreads();
         if (it >= total) break;
-        scan_strip<SW, RB, NT, SMODE>(S, it / S.S, it % S.S, sM, sV, sG, &alive);
+        scan_strip<SW, RB, NT, SMODE, MM>(S, it / S.S, it % S.S, sM, sV, &alive);
     }
 }
 
@@ -1520,12 +1506,13 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
             if (g.sliding) {   // OpenCV's running box sums: strip wavefront
-                // strips of 64 columns x blocks of 8 rows, 512 threads (DVC_OF_SCAN=64x8x256: 256 threads)
+                // strips of 64 columns x blocks of 12 rows (box radius m <= 4: winsize <= 9,
+                // the reference's) or 8, 512 threads (DVC_OF_SCAN=256: 256 threads)
                 static const int scan_cfg = [] {
                     const char* e = getenv("DVC_OF_SCAN");
-                    return e && !strcmp(e, "64x8x256") ? 1 : 0;
+                    return e && !strcmp(e, "256") ? 1 : 0;
                 }();
-                const int sw = 64, rb = 8;
+                const int sw = 64, rb = g.m <= 4 ? 12 : 8;
                 ScanArgs S{};
                 S.f = A;
                 S.S = (L.w + sw - 1) / sw;
@@ -1546,13 +1533,17 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
                 const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
-                switch (scan_cfg * 2 + (S.f.src_mode == 2)) {
-#define DVC_SCAN_CASE(i, NTv, SM) \
-    case i: hipLaunchKernelGGL((k_flow_scan<64, 8, NTv, SM>), dim3(grid_s), dim3(NTv), lds_b, s, S); break;
-                    DVC_SCAN_CASE(0, 512, 0)
-                    DVC_SCAN_CASE(1, 512, 2)
-                    DVC_SCAN_CASE(2, 256, 0)
-                    DVC_SCAN_CASE(3, 256, 2)
+                switch (scan_cfg * 4 + (rb == 12) * 2 + (S.f.src_mode == 2)) {
+#define DVC_SCAN_CASE(i, NTv, RBv, SM, MMv) \
+    case i: hipLaunchKernelGGL((k_flow_scan<64, RBv, NTv, SM, MMv>), dim3(grid_s), dim3(NTv), lds_b, s, S); break;
+                    DVC_SCAN_CASE(0, 512, 8, 0, OF_MAX_BOX_M)
+                    DVC_SCAN_CASE(1, 512, 8, 2, OF_MAX_BOX_M)
+                    DVC_SCAN_CASE(2, 512, 12, 0, 4)
+                    DVC_SCAN_CASE(3, 512, 12, 2, 4)
+                    DVC_SCAN_CASE(4, 256, 8, 0, OF_MAX_BOX_M)
+                    DVC_SCAN_CASE(5, 256, 8, 2, OF_MAX_BOX_M)
+                    DVC_SCAN_CASE(6, 256, 12, 0, 4)
+                    DVC_SCAN_CASE(7, 256, 12, 2, 4)
 #undef DVC_SCAN_CASE
                 }
             } else if (g.m == 4) {
