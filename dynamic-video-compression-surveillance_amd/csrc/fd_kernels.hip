@@ -101,17 +101,33 @@ template <int NW>
 __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
                                                    int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
-                                                   int W, int H, int WW, int ithresh)
+                                                   int W, int H, int WW, int ithresh, int xcd_bands)
 {
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H;
+    // XCD bands: blocks b, b+8, .. share an XCD (and its L2); the bijective remap
+    // below deals each such group a contiguous run of (chunk, tile row, tile)
+    // ids, so a tile's halo rows and halo quads are mostly its own XCD's lines
+    // (the default raster gives an XCD a tile column: every left/right halo
+    // quad then costs two 128-B lines fetched by another XCD)
+    int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (xcd_bands) {
+        const int nwg = gridDim.x * gridDim.y * gridDim.z;
+        const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int q = nwg >> 3, r = nwg & 7, xcd = L & 7;
+        const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+        const int T = gridDim.x * gridDim.y;
+        bz = id / T;
+        by = (id - bz * T) / gridDim.x;
+        bx = id - bz * T - by * gridDim.x;
+    }
+    const int x0 = bx * FT_W, y0 = by * FT_H;
     const int x = x0 + 4 * lane;
     const size_t mstride = (size_t)H * WW;
-    const int t_first = blockIdx.z * chunk, t_end = min(n, t_first + chunk);
-    const int t_begin = blockIdx.z == 0 ? 0 : t_first - 1;   // warm-up frame for c > 0
+    const int t_first = bz * chunk, t_end = min(n, t_first + chunk);
+    const int t_begin = bz == 0 ? 0 : t_first - 1;   // warm-up frame for c > 0
     const u16x2 bias = (u16x2)(unsigned short)(0x7fff - ithresh);   // ithresh in -1..255
 
     // Every load below is unconditional from a clamped, always-valid address
@@ -812,8 +828,11 @@ __device__ __forceinline__ void store_row(uint8_t* dst, const uint32_t* w, int b
 {
     if (!bytes) {
         uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+        // nontemporal: the output frames are never re-read by the pipeline and
+        // would otherwise evict lines the other stages re-read from L2 and the
+        // Infinity Cache (+4 % end to end, interleaved A/B at 1080p x 383)
 #pragma unroll
-        for (int d = 0; d < ND; ++d) o[d] = w[d];
+        for (int d = 0; d < ND; ++d) __builtin_nontemporal_store(w[d], o + d);
     } else {
 #pragma unroll
         for (int d = 0; d < 4 * ND; ++d) dst[d] = (uint8_t)(w[d >> 2] >> (8 * (d & 3)));
@@ -1245,8 +1264,9 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, int n
     chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
+    static const int xcd = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : 0; }();
     hipLaunchKernelGGL(k_front<NW>, dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
-                       gray_out, gs, mbits, g.W, g.H, g.WW, ithresh);
+                       gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
 }
 
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,

@@ -34,19 +34,25 @@ from . import video_io
 from .of import OFWorker
 
 
+LOG_FORMAT = "%(asctime)s - %(levelname)s - %(message)s"
+
+
+def _file_sinks(logger) -> set:
+    return {h.baseFilename for h in logger.handlers if isinstance(h, logging.FileHandler)}
+
+
 def setup_logging(output_dir):
-    """of:8-27: add a processing.log file handler (keeping any existing handlers)."""
+    """of:8-27 behaviour: the root logger gets one truncating ``processing.log``
+    sink per folder, at INFO; handlers installed by others (the GUI's) stay."""
     os.makedirs(output_dir, exist_ok=True)
-    log_file = os.path.join(output_dir, "processing.log")
-    logger = logging.getLogger()
-    exists = any(isinstance(h, logging.FileHandler) and h.baseFilename == os.path.abspath(log_file)
-                 for h in logger.handlers)
-    if not exists:
-        fh = logging.FileHandler(log_file, mode='w')
-        fh.setFormatter(logging.Formatter("%(asctime)s - %(levelname)s - %(message)s"))
-        logger.addHandler(fh)
-    logger.setLevel(logging.INFO)
-    logger.info(f"Logging configured. Log file saved in: {log_file}")
+    target = os.path.join(output_dir, "processing.log")
+    root = logging.getLogger()
+    if os.path.abspath(target) not in _file_sinks(root):
+        sink = logging.FileHandler(target, mode="w")
+        sink.setFormatter(logging.Formatter(LOG_FORMAT))
+        root.addHandler(sink)
+    root.setLevel(logging.INFO)
+    root.info(f"Logging configured. Log file saved in: {target}")
 
 
 def _device() -> int:
