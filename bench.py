@@ -153,6 +153,9 @@ def main():
                     help="independent feeds per GPU, one handle and one host thread each (config 4's unit)")
     ap.add_argument("--of-direct", action="store_true",
                     help="OF: direct per-pixel box sums (DVC_FLAG_OF_DIRECT_SUMS) instead of OpenCV's running sums")
+    ap.add_argument("--in-format", choices=("BGR", "I420", "NV12"), default="BGR",
+                    help="FD frames as decoder surfaces: 4:2:0 YUV converted on the GPU in the worker's front "
+                         "stage (cvtColor YUV2BGR, what VideoCapture.read() returns; video I/O, SURVEY §8f #1)")
     ap.add_argument("--cpu-cores", type=int, default=1,
                     help="CPU baseline: this many feeds on this many host processes (1 = single core)")
     args = ap.parse_args()
@@ -186,20 +189,34 @@ def main():
 
     # per feed: its own synthetic camera (seed = global feed index); frame j of
     # a step is ring frame order[(j + 1) % P] (frame 0 primes the feed)
+    yuv = args.in_format != "BGR" and not of
+
+    def to_surface(fr):
+        """BGR -> the 4:2:0 surface a decoder would hand over (cvtColor BGR2YUV_I420 on the GPU)."""
+        i420 = dvc_amd._native.bgr_to_i420(fr, local)
+        if args.in_format == "NV12":
+            c = i420[H:].reshape(-1)
+            u, v = c[:H * W // 4].reshape(H // 2, W // 2), c[H * W // 4:].reshape(H // 2, W // 2)
+            i420 = np.concatenate([i420[:H], np.stack([u, v], -1).reshape(H // 2, W)])
+        return i420
+
     def feed_inputs(f):
         clip = SyntheticClip(W, H, seed=rank * F + f, noisy=args.noisy)
         ring = [clip.frame(i) for i in range(R)]
+        if yuv:
+            ring = [to_surface(fr) for fr in ring]
+        fshape = ring[0].shape
         idx = [order[(j + 1) % P] for j in range(P)]
         oshape = (P, H, W) if of else (P, H, W, 3)     # OF writes a mask plane instead of the red overlay
         if args.io == "device":
-            seq = torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev)
+            seq = torch.empty((P,) + fshape, dtype=torch.uint8, device=dev)
             for j in range(P):
                 seq[j].copy_(torch.from_numpy(ring[idx[j]]))
             outs = (torch.empty(oshape, dtype=torch.uint8, device=dev),
                     torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev))
         else:
             alloc = dvc_amd._native.pinned if args.io == "host-pinned" else (lambda shp: np.empty(shp, np.uint8))
-            seq = alloc((P, H, W, 3))
+            seq = alloc((P,) + fshape)
             for j in range(P):
                 seq[j] = ring[idx[j]]
             outs = (alloc(oshape), alloc((P, H, W, 3)))
@@ -212,7 +229,7 @@ def main():
     def make_worker(f, ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
         kw = dict(direct_sums=args.of_direct) if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
-                                release_factor=args.release_factor)
+                                release_factor=args.release_factor, in_format=args.in_format)
         w = cls(W, H, device=local, device_ptrs=not host_io, ktiming=ktiming, max_batch=batch, **kw)
         w.prime(inputs[f][2])
         return w
@@ -297,6 +314,8 @@ def main():
             workload += f"_{args.io}_io"
         if args.per_frame:
             workload += "_per_frame"
+        if yuv:
+            workload += f"_{args.in_format.lower()}_input"
         if of and args.of_direct:
             workload += "_direct_sums"
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
@@ -332,7 +351,7 @@ def main():
                        else "frame-differencing (frame_differencing.py)",
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": F,
                        "io": args.io + (" (PCIe-inclusive: frames up, both outputs down)" if host_io else ""),
-                       "ring_frames": R, "noisy": args.noisy,
+                       "ring_frames": R, "noisy": args.noisy, "in_format": "BGR" if of else args.in_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),

@@ -16,8 +16,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
-SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip"]
-HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h"]
+SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip", "yuv_kernels.hip"]
+HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h", "yuv_kernels.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 DVC_OK = 0
@@ -27,6 +27,8 @@ DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
 DVC_FLAG_JOIN_STREAM = 0x8
 DVC_FLAG_OF_DIRECT_SUMS = 0x10
+FMT_BGR, FMT_I420, FMT_NV12 = 0, 1, 2      # DVC_FMT_* frame formats (video I/O)
+FORMATS = {"BGR": FMT_BGR, "I420": FMT_I420, "NV12": FMT_NV12}
 
 PLANE_GRAY, PLANE_MOTION, PLANE_FILTERED, PLANE_ACC, PLANE_DILATED = range(5)
 OF_PLANE_RAW, OF_PLANE_SMOOTH, OF_PLANE_MORPH, OF_PLANE_RECT, OF_PLANE_GRAY = range(5)
@@ -38,9 +40,9 @@ EXPORTS = [
     "dvc_fd_destroy", "dvc_gaussian_taps_q8", "dvc_contour_filter", "dvc_fd_step_batch",
     "dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync", "dvc_of_get_stats",
     "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
-    "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free",
+    "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free", "dvc_yuv420_to_bgr", "dvc_bgr_to_i420",
 ]
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_BATCH = 512
 
 
@@ -71,6 +73,8 @@ class FdParams(ctypes.Structure):
         ("max_batch", ctypes.c_uint32),
         ("src_width", ctypes.c_int32),
         ("src_height", ctypes.c_int32),
+        ("in_format", ctypes.c_int32),
+        ("chroma_rows", ctypes.c_int32),
     ]
 
 
@@ -186,6 +190,14 @@ def lib() -> ctypes.CDLL:
     L.dvc_host_alloc.restype = ctypes.c_int
     L.dvc_host_free.argtypes = [vp]
     L.dvc_host_free.restype = None
+    L.dvc_yuv420_to_bgr.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                    vp, ctypes.c_uint32]
+    L.dvc_bgr_to_i420.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, vp,
+                                  ctypes.c_uint32]
+    L.dvc_yuv420_to_bgr.restype = ctypes.c_int
+    L.dvc_bgr_to_i420.restype = ctypes.c_int
     for name in ("dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync",
                  "dvc_of_get_stats", "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_compress"):
         getattr(L, name).restype = ctypes.c_int
@@ -256,6 +268,38 @@ def of_compress(bgr, mask, quant: float = 100.0, device: int = 0):
     check(lib().dvc_of_compress(f.ctypes.data, 3 * W, m.ctypes.data, W, H, float(quant), int(device),
                                 out.ctypes.data))
     return out
+
+
+def yuv420_to_bgr(frames, fmt: str = "I420", device: int = 0):
+    """cv2.cvtColor(COLOR_YUV2BGR_I420 / _NV12) on the GPU of host 4:2:0 frames:
+    one (H*3/2, W) uint8 frame or an (n, H*3/2, W) stack -> (.., H, W, 3) BGR."""
+    import numpy as np
+    f = np.ascontiguousarray(frames, dtype=np.uint8)
+    one = f.ndim == 2
+    f = f[None] if one else f
+    n, H, W = f.shape[0], f.shape[1] * 2 // 3, f.shape[2]
+    if f.shape[1] != H * 3 // 2 or H % 2 or W % 2:
+        raise ValueError(f"4:2:0 frames must be (H*3/2, W) with H, W even, got {f.shape[1:]}")
+    out = np.empty((n, H, W, 3), np.uint8)
+    check(lib().dvc_yuv420_to_bgr(f.ctypes.data, W, FORMATS[fmt], 0, W, H, n, f[0].nbytes, out.ctypes.data, 3 * W,
+                                  3 * W * H, int(device), None, 0))
+    return out[0] if one else out
+
+
+def bgr_to_i420(frames, device: int = 0):
+    """cv2.cvtColor(COLOR_BGR2YUV_I420) on the GPU of host BGR frames: (H, W, 3) or
+    (n, H, W, 3) uint8 -> (.., H*3/2, W) I420."""
+    import numpy as np
+    f = np.ascontiguousarray(frames, dtype=np.uint8)
+    one = f.ndim == 3
+    f = f[None] if one else f
+    n, H, W = f.shape[:3]
+    if H % 2 or W % 2 or f.shape[3] != 3:
+        raise ValueError(f"BGR frames must be (H, W, 3) with H, W even, got {f.shape[1:]}")
+    out = np.zeros((n, H * 3 // 2, W), np.uint8)
+    check(lib().dvc_bgr_to_i420(f.ctypes.data, 3 * W, 3 * W * H, W, H, n, out.ctypes.data, W, 0, out[0].nbytes,
+                                int(device), None, 0))
+    return out[0] if one else out
 
 
 def gaussian_taps_q8(n: int, sigma: float) -> list:

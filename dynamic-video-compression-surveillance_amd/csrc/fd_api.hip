@@ -19,6 +19,7 @@
 #include "../../include/dvc.h"
 #include "fd_kernels.h"
 #include "host_common.h"
+#include "yuv_kernels.h"
 
 namespace dvc_host {
 
@@ -113,7 +114,8 @@ struct Slot {
     dvc::CclBufs c{};
     uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;    // fast back end (B = 4, 8)
     uint64_t *dbits = nullptr, *rbits = nullptr, *zbits = nullptr;  // generic back end (row-major planes)
-    uint8_t* fin = nullptr;    // resized / re-pitched input frames (pitch ip), allocated when needed
+    uint8_t* fin = nullptr;    // resized / re-pitched / converted input frames (pitch ip), allocated when needed
+    uint8_t* fsrc = nullptr;   // YUV frames converted to BGR at the source size, before the resize (pitch sip)
     hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_acc = nullptr, ev_out = nullptr;
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
 };
@@ -152,6 +154,8 @@ struct dvc_fd {
     int sw = 0, sh = 0;  // source frame size (resized to W x H when different)
     int sip = 0;         // pitch of staged source frames (host path): 3 * roundup(sw, 4)
     bool resize = false;
+    int fmt = DVC_FMT_BGR;  // frame format handed to prime/step (DVC_FMT_*)
+    int crows = 0;          // YUV: luma rows before the chroma planes (device-pointer frames)
     dvc::ResizeTab rt{};
     int B = 4, NBX = 0, NBY = 0, AP = 0;   // block size, blocks (ceil), acc pitch
     bool fast = true;                      // B = 4, 8: block-field back end
@@ -189,7 +193,7 @@ static void free_all(dvc_fd* h)
 {
     for (Slot& s : h->slot) {
         void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE,
-                       s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin};
+                       s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin, s.fsrc};
         for (void* p : dev)
             if (p) (void)hipFree(p);
         for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_acc, s.ev_out})
@@ -270,7 +274,7 @@ static int check_stop(dvc_fd* h)
 // Can the kernels read these frames in place? (dword rows reaching 3 * gs bytes)
 static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
-    return !h->resize && pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 &&
+    return h->fmt == DVC_FMT_BGR && !h->resize && pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 &&
            (n <= 1 || fstride % 4 == 0);
 }
 
@@ -287,9 +291,40 @@ static bool host_pinned(const void* p)
 static hipError_t alloc_fin(dvc_fd* h)
 {
     hipError_t e = hipSuccess;
-    for (Slot& s : h->slot)
+    for (Slot& s : h->slot) {
         if (!s.fin && e == hipSuccess) e = dalloc(&s.fin, (size_t)h->ip * h->g.H * h->max_batch);
+        if (!s.fsrc && h->fmt != DVC_FMT_BGR && h->resize && e == hipSuccess)
+            e = dalloc(&s.fsrc, (size_t)h->sip * h->sh * h->max_batch);
+    }
     return e;
+}
+
+// Bytes a frame handed to prime/step spans (rows of `pitch`): BGR rows, or a
+// YUV 4:2:0 frame's luma + chroma planes (include/dvc.h frame layout).
+static size_t frame_span(const dvc_fd* h, size_t pitch, int crows)
+{
+    if (h->fmt == DVC_FMT_BGR) return pitch * (h->sh - 1) + 3 * (size_t)h->sw;
+    return dvc::yuv_frame_bytes(pitch, crows);
+}
+
+// Copy host frame `src` into pinned staging `dst` in the compact layout the
+// staged device copy is read with (BGR rows of sip; YUV: luma rows of sw and
+// the chroma plane(s) right after them).
+static void pack_host_frame(const dvc_fd* h, const uint8_t* src, size_t pitch, uint8_t* dst)
+{
+    const size_t sw = h->sw, sh = h->sh;
+    if (h->fmt == DVC_FMT_BGR) {
+        for (size_t y = 0; y < sh; ++y) std::memcpy(dst + y * h->sip, src + y * pitch, 3 * sw);
+        return;
+    }
+    const dvc::YuvLayout L = dvc::yuv_layout(src, pitch, h->fmt, h->crows, 0);
+    const dvc::YuvLayout C = dvc::yuv_layout(dst, sw, h->fmt, (int)sh, 0);
+    for (size_t y = 0; y < sh; ++y) std::memcpy(dst + y * sw, src + y * pitch, sw);
+    const size_t cb = h->fmt == DVC_FMT_NV12 ? sw : sw / 2;   // chroma bytes per row and plane
+    for (size_t y = 0; y < sh / 2; ++y) {
+        std::memcpy(dst + C.uoff + y * C.cpitch, src + L.uoff + y * L.cpitch, cb);
+        if (h->fmt == DVC_FMT_I420) std::memcpy(dst + C.voff + y * C.cpitch, src + L.voff + y * L.cpitch, cb);
+    }
 }
 
 extern "C" {
@@ -339,6 +374,14 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         return fail(DVC_E_INVALID, "dilation kernel %d (anchor %d) outside 1..63", p.ksize, p.anchor);
     if (p.ithresh < -1 || p.ithresh > 255) return fail(DVC_E_INVALID, "ithresh %d outside -1..255", p.ithresh);
     if (!(p.quant == p.quant) || p.quant == 0.0f) return fail(DVC_E_INVALID, "quantization_level must be nonzero");
+    if (p.in_format != DVC_FMT_BGR && p.in_format != DVC_FMT_I420 && p.in_format != DVC_FMT_NV12)
+        return fail(DVC_E_INVALID, "in_format %d unknown", p.in_format);
+    if (p.in_format != DVC_FMT_BGR) {
+        const int sw = p.src_width ? p.src_width : p.width, sh = p.src_height ? p.src_height : p.height;
+        if ((sw & 1) || (sh & 1)) return fail(DVC_E_INVALID, "4:2:0 frames %dx%d: sides must be even", sw, sh);
+        if (p.chroma_rows && (p.chroma_rows < sh || (p.chroma_rows & 1)))
+            return fail(DVC_E_INVALID, "chroma_rows %d: even and >= the frame height %d", p.chroma_rows, sh);
+    }
     const int mb = p.max_batch == 0 ? 1 : (int)p.max_batch;
     if (p.max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %u outside 1..%d", p.max_batch, DVC_MAX_BATCH);
     dvc_fd* h = new dvc_fd();
@@ -355,6 +398,8 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->sh = p.src_height ? p.src_height : p.height;
     h->sip = 3 * ((h->sw + 3) & ~3);
     h->resize = h->sw != p.width || h->sh != p.height;
+    h->fmt = p.in_format;
+    h->crows = p.chroma_rows ? p.chroma_rows : h->sh;
     h->B = p.block;
     h->fast = dvc::fast_block(p.block);
     h->NBX = (p.width + p.block - 1) / p.block;
@@ -420,7 +465,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
     // staged input frames: always needed to resize or when rows are not whole quads
-    if (h->resize || p.width % 4) {
+    if (h->resize || p.width % 4 || h->fmt != DVC_FMT_BGR) {
         if ((e = alloc_fin(h)) != hipSuccess) return bad(e, "hipMalloc");
     }
     const size_t accb = (size_t)h->AP * h->NBY * p.block;
@@ -503,7 +548,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
 // buffer on s_front (re-pitched, or resized — cv2.resize, fd:74,91). The
 // staged buffer is rewritten only after the slot's previous batch is out.
 static int stage_input(dvc_fd* h, Slot& S, const uint8_t* src, size_t pitch, size_t fstride, int n,
-                       const uint8_t** d, int* dp, size_t* dfs)
+                       const uint8_t** d, int* dp, size_t* dfs, int crows)
 {
     if (direct_frames(h, src, pitch, fstride, n)) {
         *d = src;
@@ -514,7 +559,15 @@ static int stage_input(dvc_fd* h, Slot& S, const uint8_t* src, size_t pitch, siz
     if (!S.fin) HIP_OK(alloc_fin(h));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
     const size_t H = h->g.H, fs = (size_t)h->ip * H;
-    if (h->resize) {
+    if (h->fmt != DVC_FMT_BGR) {
+        // the decoder's 4:2:0 surfaces -> BGR (cvtColor, what VideoCapture.read()
+        // returns, fd:87), at the source size when a resize follows
+        const dvc::YuvLayout L = dvc::yuv_layout(src, pitch, h->fmt, crows, fstride);
+        const size_t sfs = (size_t)h->sip * h->sh;
+        HIP_OK(dvc::launch_yuv420_to_bgr(L, h->sw, h->sh, n, h->resize ? S.fsrc : S.fin, h->resize ? h->sip : h->ip,
+                                         h->resize ? sfs : fs, h->s_front));
+        if (h->resize) HIP_OK(dvc::launch_resize(S.fsrc, h->sip, sfs, S.fin, h->ip, fs, n, h->rt, h->s_front));
+    } else if (h->resize) {
         HIP_OK(dvc::launch_resize(src, (int)pitch, fstride, S.fin, h->ip, fs, n, h->rt, h->s_front));
     } else if (n == 1 || fstride == pitch * H) {
         HIP_OK(hipMemcpy2DAsync(S.fin, h->ip, src, pitch, 3 * (size_t)h->g.W, H * n, hipMemcpyDeviceToDevice,
@@ -535,7 +588,9 @@ extern "C" {
 int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 {
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
-    if (pitch < 3 * (size_t)h->sw) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (pitch < (h->fmt == DVC_FMT_BGR ? 3 * (size_t)h->sw : (size_t)h->sw) ||
+        (h->fmt == DVC_FMT_I420 && (pitch & 1)))
+        return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
     const size_t W = h->p.width, H = h->p.height;
     if (!h->tmp32) {
@@ -548,17 +603,19 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
     for (Stage& s : h->stage) s.busy = false;
     const uint8_t* src = bgr;
     size_t sp = pitch;
+    int crows = h->crows;
     if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
         Stage& st = h->stage[0];
-        for (int y = 0; y < h->sh; ++y) std::memcpy(st.h_in + (size_t)y * h->sip, bgr + y * pitch, 3 * (size_t)h->sw);
+        pack_host_frame(h, bgr, pitch, st.h_in);
         HIP_OK(hipMemcpyAsync(st.d_in, st.h_in, (size_t)h->sip * h->sh, hipMemcpyHostToDevice, h->s_front));
         src = st.d_in;
-        sp = h->sip;
+        sp = h->fmt == DVC_FMT_BGR ? h->sip : h->sw;
+        crows = h->sh;
     }
     const uint8_t* d = nullptr;
     int dp = 0;
     size_t dfs = 0;
-    int rc = stage_input(h, h->slot[0], src, sp, 0, 1, &d, &dp, &dfs);
+    int rc = stage_input(h, h->slot[0], src, sp, 0, 1, &d, &dp, &dfs, crows);
     if (rc) return rc;
     HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->gcur], h->p.width, h->p.height, h->gs, h->kprime,
                              h->s_front));
@@ -587,7 +644,7 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
 // output of i-1 can all be in flight; the two recurrences (previous gray,
 // accumulated mask) are serial, each on its own stream.
 static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
-                         size_t ostride)
+                         size_t ostride, int crows)
 {
     Slot& S = h->slot[h->seq % NSLOT];
     hipStream_t s_ccl = h->stream;
@@ -595,7 +652,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     const uint8_t* d = nullptr;
     int dp = 0;
     size_t dfs = 0;
-    int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs);
+    int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs, crows);
     if (rc) return rc;
     HIP_OK(dvc::launch_front(d, dp, dfs, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
                              h->p.ithresh, h->s_front));
@@ -703,8 +760,10 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
                                (unsigned long long)h->err_frame + 1);
     if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
     const size_t W = h->p.width, H = h->p.height, N = W * H, srow = 3 * (size_t)h->sw;
-    if (pitch < srow) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    if (n > 1 && fstride < pitch * (h->sh - 1) + srow) return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
+    const bool yuv = h->fmt != DVC_FMT_BGR;
+    if (pitch < (yuv ? (size_t)h->sw : srow) || (h->fmt == DVC_FMT_I420 && (pitch & 1)))
+        return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (n > 1 && fstride < frame_span(h, pitch, h->crows)) return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
     if (n > 1 && (overlay || compressed) && ostride < 3 * N)
         return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
@@ -715,14 +774,14 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
             const int m = std::min(h->max_batch, n - f0);
             int rc = enqueue_batch(h, bgr + (size_t)f0 * fstride, pitch, fstride, m,
                                    overlay ? overlay + (size_t)f0 * ostride : nullptr,
-                                   compressed ? compressed + (size_t)f0 * ostride : nullptr, ostride);
+                                   compressed ? compressed + (size_t)f0 * ostride : nullptr, ostride, h->crows);
             if (rc) return rc;
         }
         if (acc_out) HIP_OK(hipMemcpy2DAsync(acc_out, W, h->acc, h->AP, W, H, hipMemcpyDeviceToDevice, h->s_acc));
         HIP_OK(join_user(h));
         return DVC_OK;
     }
-    const bool pin_in = host_pinned(bgr);
+    const bool pin_in = !yuv && host_pinned(bgr);   // YUV frames are repacked on the host
     const bool pin_out = (!overlay || host_pinned(overlay)) && (!compressed || host_pinned(compressed));
     const size_t N3 = 3 * N, sfs = (size_t)h->sip * h->sh;
     for (int f0 = 0; f0 < n; f0 += h->max_batch) {
@@ -741,14 +800,12 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
                                         hipMemcpyHostToDevice, h->s_front));
         } else {
             HIP_OK(hipEventSynchronize(st.ev_h2d));   // h_in's previous upload is done
-            for (int t = 0; t < m; ++t)
-                for (int y = 0; y < h->sh; ++y)
-                    std::memcpy(st.h_in + t * sfs + (size_t)y * h->sip, in + (size_t)t * fstride + (size_t)y * pitch,
-                                srow);
+            for (int t = 0; t < m; ++t) pack_host_frame(h, in + (size_t)t * fstride, pitch, st.h_in + t * sfs);
             HIP_OK(hipMemcpyAsync(st.d_in, st.h_in, (size_t)m * sfs, hipMemcpyHostToDevice, h->s_front));
             HIP_OK(hipEventRecord(st.ev_h2d, h->s_front));
         }
-        rc = enqueue_batch(h, st.d_in, h->sip, sfs, m, ov ? st.d_ov : nullptr, cp ? st.d_cp : nullptr, N3);
+        rc = enqueue_batch(h, st.d_in, yuv ? h->sw : h->sip, sfs, m, ov ? st.d_ov : nullptr, cp ? st.d_cp : nullptr, N3,
+                           h->sh);
         if (rc) return rc;
         if (pin_out) {
             if (ov) HIP_OK(hipMemcpy2DAsync(ov, ostride, st.d_ov, N3, N3, m, hipMemcpyDeviceToHost, h->s_out));

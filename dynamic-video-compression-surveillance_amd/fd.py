@@ -22,7 +22,7 @@ from . import _native as N
 def derive_params(width: int, height: int, block_size: int = 4, motion_threshold: float = 0.5,
                   min_area: float = 500, kernel_size: int = 7, release_factor: float = 0.5,
                   quantization_level: float = 100, flags: int = 0, src_width: int = 0,
-                  src_height: int = 0) -> N.FdParams:
+                  src_height: int = 0, in_format: str = "BGR", chroma_rows: int = 0) -> N.FdParams:
     """dvc_fd_params from the reference kwargs (frame_differencing.py:21-30).
 
     * ``ithresh = floor(motion_threshold)`` clamped to [-1, 255]: cv::threshold
@@ -47,6 +47,8 @@ def derive_params(width: int, height: int, block_size: int = 4, motion_threshold
     p.prime_sigma = 30.0
     p.flags = flags
     p.src_width, p.src_height = int(src_width or 0), int(src_height or 0)
+    p.in_format = N.FORMATS[in_format]
+    p.chroma_rows = int(chroma_rows)
     return p
 
 
@@ -68,6 +70,7 @@ class FDWorker:
         self.W, self.H = int(width), int(height)
         self.SW = int(kwargs.get("src_width") or width)
         self.SH = int(kwargs.get("src_height") or height)
+        self.in_format = kwargs.get("in_format", "BGR")
         self.device = int(device)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
@@ -79,8 +82,12 @@ class FDWorker:
     # -------------------------------------------------------------- frames --
     @property
     def _fshape(self):
-        """Input frames (source size)."""
-        return (self.SH, self.SW, 3)
+        """Input frames (source size): packed BGR, or a (H*3/2, W) 4:2:0 frame."""
+        return (self.SH, self.SW, 3) if self.in_format == "BGR" else (self.SH * 3 // 2, self.SW)
+
+    @property
+    def _pitch(self):
+        return 3 * self.SW if self.in_format == "BGR" else self.SW
 
     @property
     def _oshape(self):
@@ -95,10 +102,10 @@ class FDWorker:
         """fd:67-81: previous gray := GaussianBlur(gray(frame), 25x25, 30); acc := 0."""
         if self.device_ptrs:
             addr, _ = self._dev(frame, "frame")
-            N.check(self._lib.dvc_fd_prime(self._h, addr, 3 * self.SW))
+            N.check(self._lib.dvc_fd_prime(self._h, addr, self._pitch))
         else:
             f = B.host_in(frame, self._fshape, "frame")
-            N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, 3 * self.SW))
+            N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, self._pitch))
 
     def step(self, frame, overlay=None, compressed=None, acc=None, want=("overlay", "compressed")):
         """fd:91-133 for one frame.
@@ -112,13 +119,13 @@ class FDWorker:
             ov = self._dev(overlay, "overlay", tail=self._oshape)[0] if overlay is not None else None
             cp = self._dev(compressed, "compressed", tail=self._oshape)[0] if compressed is not None else None
             ac = self._dev(acc, "acc", tail=(self.H, self.W))[0] if acc is not None else None
-            N.check(self._lib.dvc_fd_step(self._h, addr, 3 * self.SW, ov, cp, ac))
+            N.check(self._lib.dvc_fd_step(self._h, addr, self._pitch, ov, cp, ac))
             return None
         f = B.host_in(frame, self._fshape, "frame")
         overlay = B.host_out(overlay, self._oshape, "overlay", "overlay" in want)
         compressed = B.host_out(compressed, self._oshape, "compressed", "compressed" in want)
         acc = B.host_out(acc, (self.H, self.W), "acc", False)
-        N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, 3 * self.SW,
+        N.check(self._lib.dvc_fd_step(self._h, f.ctypes.data, self._pitch,
                                       overlay.ctypes.data if overlay is not None else None,
                                       compressed.ctypes.data if compressed is not None else None,
                                       acc.ctypes.data if acc is not None else None))
@@ -134,21 +141,21 @@ class FDWorker:
         handle's device (outputs may hold more frames), or explicit
         ``(address, n)`` tuples of dense frames; asynchronous, returns None.
         """
-        fs, os_ = 3 * self.SW * self.SH, 3 * self.W * self.H
+        fs, os_ = int(np.prod(self._fshape)), 3 * self.W * self.H
         if self.device_ptrs:
             addr, n = self._dev(frames, "frames", batched=True)
             ov = self._dev(overlay, "overlay", n=n, batched=True, tail=self._oshape)[0] if overlay is not None else None
             cp = self._dev(compressed, "compressed", n=n, batched=True, tail=self._oshape)[0] \
                 if compressed is not None else None
-            N.check(self._lib.dvc_fd_step_batch(self._h, addr, 3 * self.SW, fs, n, ov, cp, os_))
+            N.check(self._lib.dvc_fd_step_batch(self._h, addr, self._pitch, fs, n, ov, cp, os_))
             return None
-        if not isinstance(frames, np.ndarray) or frames.ndim != 4:
-            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.SH}, {self.SW}, 3)")
+        if not isinstance(frames, np.ndarray) or frames.ndim != len(self._fshape) + 1:
+            raise ValueError(f"frames: expected uint8 frames of shape (n, {', '.join(map(str, self._fshape))})")
         n = int(frames.shape[0])
         f = B.host_in(frames, (n,) + self._fshape, "frames")
         overlay = B.host_out(overlay, (n,) + self._oshape, "overlay", "overlay" in want)
         compressed = B.host_out(compressed, (n,) + self._oshape, "compressed", "compressed" in want)
-        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, 3 * self.SW, fs, n,
+        N.check(self._lib.dvc_fd_step_batch(self._h, f.ctypes.data, self._pitch, fs, n,
                                             overlay.ctypes.data if overlay is not None else None,
                                             compressed.ctypes.data if compressed is not None else None, os_))
         return overlay, compressed

@@ -104,7 +104,11 @@ def filter_and_dilate_movements(video_path, output_dir,
     out_w, out_h = int(src_w * scale_factor), int(src_h * scale_factor)   # fd:60-61
     sinks = _Writers(out_dir, fps, (out_w, out_h), progress_callback)
 
-    ok, first = cap.read()
+    # a 4:2:0 source (Y4M; a hardware decoder's surfaces) goes to the worker as
+    # is: it converts on the GPU exactly as VideoCapture.read() would (fd:87)
+    yuv = getattr(cap, "pixel_format", "BGR") != "BGR"
+    read = cap.read_yuv if yuv else cap.read
+    ok, first = read()
     if not ok:
         logging.error("Unable to read the first frame of the video.")
         cap.release()
@@ -117,16 +121,16 @@ def filter_and_dilate_movements(video_path, output_dir,
         worker = FDWorker(out_w, out_h, device=_device(), src_width=src_w, src_height=src_h, max_batch=R,
                           block_size=block_size, motion_threshold=motion_threshold, min_area=min_area,
                           kernel_size=kernel_size, release_factor=release_factor,
-                          quantization_level=quantization_level)
+                          quantization_level=quantization_level, in_format=cap.pixel_format if yuv else "BGR")
         worker.prime(first)                                     # fd:67-81 (resize on the GPU)
-        frames = pinned((R, src_h, src_w, 3))
+        frames = pinned((R,) + worker._fshape)
         overlay, compressed = pinned((R, out_h, out_w, 3)), pinned((R, out_h, out_w, 3))
         eof = False
         while not eof:
             t0 = time.time()
             n = 0
             while n < R:                                        # fd:87-89
-                ok, f = cap.read()
+                ok, f = read()
                 if not ok:
                     eof = True
                     break

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 4
+#define DVC_ABI_VERSION 5
 #define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
@@ -69,6 +69,37 @@ extern "C" {
 #define DVC_FLAG_OF_DIRECT_SUMS 0x10u /* OF: direct per-pixel 9x9 box sums instead
                                      of OpenCV's running sums (the default,
                                      FarnebackUpdateFlow_Blur's order)          */
+
+/* ---- frame formats (video I/O) ----------------------------- */
+/* What the worker's frames are. The reference's are packed BGR straight from
+ * cv2.VideoCapture.read() (fd:87); a hardware decoder (VCN via rocDecode) or a
+ * Y4M file yields 4:2:0 YUV, which the worker converts on the GPU exactly as
+ * cv2.cvtColor(COLOR_YUV2BGR_I420 / COLOR_YUV2BGR_NV12) does before the loop
+ * body, so a decoded surface never round-trips through the host.
+ * YUV frame layout: luma = `height` rows of `pitch` bytes; the chroma plane(s)
+ * start chroma_rows * pitch bytes after the frame's first byte (chroma_rows >=
+ * height, 0 = height: decoder surfaces pad the luma height); I420: U plane of
+ * height/2 rows of pitch/2 bytes, V plane (chroma_rows/2) * (pitch/2) bytes after
+ * U; NV12: one interleaved UV plane of height/2 rows of `pitch` bytes. A frame
+ * spans pitch * chroma_rows * 3/2 bytes. Width and height even. */
+#define DVC_FMT_BGR  0
+#define DVC_FMT_I420 1
+#define DVC_FMT_NV12 2
+
+/* Standalone conversions (the decode / encode ends of the video I/O), n frames
+ * frame_stride (YUV) / bgr_stride (BGR) bytes apart, on `device`:
+ *   dvc_yuv420_to_bgr  cv2.cvtColor(COLOR_YUV2BGR_I420 or _NV12) — what
+ *                      cv2.VideoCapture.read() hands the loop (fd:87, of:66,145)
+ *   dvc_bgr_to_i420    cv2.cvtColor(COLOR_BGR2YUV_I420) — the 4:2:0 frame an
+ *                      encoder takes from cv2.VideoWriter.write() (fd:112,131)
+ * flags: DVC_FLAG_DEVICE_PTRS = device pointers, enqueued on hip_stream (NULL:
+ * the default stream) and asynchronous; otherwise host pointers, synchronous. */
+int dvc_yuv420_to_bgr(const uint8_t* yuv, size_t pitch, int fmt, int chroma_rows, int width, int height, int n,
+                      size_t frame_stride, uint8_t* bgr, size_t bgr_pitch, size_t bgr_stride, int device,
+                      void* hip_stream, uint32_t flags);
+int dvc_bgr_to_i420(const uint8_t* bgr, size_t bgr_pitch, size_t bgr_stride, int width, int height, int n,
+                    uint8_t* yuv, size_t pitch, int chroma_rows, size_t frame_stride, int device, void* hip_stream,
+                    uint32_t flags);
 
 /* ---- frame-differencing (FD) path ------------------------------------------ */
 
@@ -117,6 +148,10 @@ typedef struct dvc_fd_params {
                            flight (3 x max_batch frames). */
     int32_t src_width;  /* 0: = width  */
     int32_t src_height; /* 0: = height */
+    int32_t in_format;  /* DVC_FMT_BGR (0) / DVC_FMT_I420 / DVC_FMT_NV12: the frames
+                           handed to prime/step (src size; YUV: `pitch` is the luma
+                           pitch, frames converted on the GPU first, fd:87) */
+    int32_t chroma_rows;/* YUV: see the frame layout above (0 = src_height) */
 } dvc_fd_params;
 
 /* Cumulative per-handle counters (all frames stepped since create/prime). */

@@ -48,6 +48,8 @@ class FdParams(ctypes.Structure):
         ("max_batch", ctypes.c_uint32),
         ("src_width", ctypes.c_int32),
         ("src_height", ctypes.c_int32),
+        ("in_format", ctypes.c_int32),
+        ("chroma_rows", ctypes.c_int32),
     ]
 
 
@@ -115,6 +117,10 @@ def lib():
         L.oc_fd_read_plane.argtypes = [ctypes.c_void_p, ctypes.c_int, u8p]
         L.oc_fd_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(FdStats)]
         L.oc_fd_set_state.argtypes = [ctypes.c_void_p, u8p, u8p]
+        L.oc_yuv420_to_bgr.argtypes = [u8p, ctypes.c_size_t, u8p, u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, u8p, ctypes.c_size_t]
+        L.oc_bgr_to_i420.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t, u8p, u8p,
+                                     ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -290,6 +296,35 @@ def resize(bgr: np.ndarray, width: int, height: int) -> np.ndarray:
     h, w = bgr.shape[:2]
     out = np.empty((int(height), int(width), 3), np.uint8)
     lib().oc_resize_bgr(_u8(bgr), 3 * w, w, h, _u8(out), 3 * int(width), int(width), int(height))
+    return out
+
+
+def yuv420_to_bgr(frame: np.ndarray, fmt: str = "I420") -> np.ndarray:
+    """cv2.cvtColor(frame, COLOR_YUV2BGR_I420 / COLOR_YUV2BGR_NV12) of a
+    (H*3/2) x W uint8 4:2:0 frame (oracle/yuv_oracle.c; parity-unpinned vs cv2)."""
+    frame = np.ascontiguousarray(frame, np.uint8)
+    H, W = frame.shape[0] * 2 // 3, frame.shape[1]
+    out = np.empty((H, W, 3), np.uint8)
+    base = frame.ctypes.data
+    p = ctypes.POINTER(ctypes.c_uint8)
+    if fmt == "NV12":
+        u, v, cp, cs = base + H * W, base + H * W + 1, W, 2
+    else:
+        u, v, cp, cs = base + H * W, base + H * W + (H // 2) * (W // 2), W // 2, 1
+    lib().oc_yuv420_to_bgr(_u8(frame), W, ctypes.cast(u, p), ctypes.cast(v, p), cp, cs, W, H, _u8(out), 3 * W)
+    return out
+
+
+def bgr_to_i420(bgr: np.ndarray) -> np.ndarray:
+    """cv2.cvtColor(bgr, COLOR_BGR2YUV_I420): a (H*3/2) x W frame (Y, then U and V
+    planes of H/2 x W/2), restated in oracle/yuv_oracle.c (parity-unpinned vs cv2)."""
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    H, W = bgr.shape[:2]
+    out = np.empty((H * 3 // 2, W), np.uint8)
+    base = out.ctypes.data
+    p = ctypes.POINTER(ctypes.c_uint8)
+    lib().oc_bgr_to_i420(_u8(bgr), 3 * W, W, H, _u8(out), W, ctypes.cast(base + H * W, p),
+                         ctypes.cast(base + H * W + (H // 2) * (W // 2), p), W // 2)
     return out
 
 

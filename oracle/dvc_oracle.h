@@ -67,4 +67,10 @@ int oc_of_prime(oc_of* h, const uint8_t* bgr, size_t pitch);
 int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_t* compressed, float* flow);
 int oc_of_read_plane(oc_of* h, int which, uint8_t* dst);
 void oc_of_set_state(oc_of* h, const uint8_t* prev_gray, const uint8_t* raw_masks, int n);
+
+/* yuv_oracle.c: 4:2:0 YUV <-> packed BGR (cvtColor YUV2BGR_I420/NV12, BGR2YUV_I420) */
+void oc_yuv420_to_bgr(const uint8_t* y, size_t ypitch, const uint8_t* u, const uint8_t* v, size_t cpitch, int cstep,
+                      int W, int H, uint8_t* bgr, size_t bpitch);
+void oc_bgr_to_i420(const uint8_t* bgr, size_t bpitch, int W, int H, uint8_t* y, size_t ypitch, uint8_t* u,
+                    uint8_t* v, size_t cpitch);
 #endif

@@ -1,0 +1,180 @@
+"""Video I/O on the GPU: the 4:2:0 <-> BGR conversion kernels
+(dvc_yuv420_to_bgr / dvc_bgr_to_i420) bit-exact against oracle/yuv_oracle.c,
+and the FD worker fed decoder-style 4:2:0 surfaces (in_format I420 / NV12,
+padded pitch and luma height, host and device pointers, batches, resize)
+bit-exact against the oracle worker run on the oracle-converted BGR frames —
+what cv2.VideoCapture.read() would hand the reference loop (fd:87). Against
+OpenCV itself the conversion is parity-unpinned (no cv2 in this image)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _i420_frames(oracle, frames):
+    return np.stack([oracle.bgr_to_i420(f) for f in frames])
+
+
+def _nv12(i420, H, W):
+    Y, rest = i420[:H], i420[H:].ravel()
+    U, V = rest[:H * W // 4].reshape(H // 2, W // 2), rest[H * W // 4:].reshape(H // 2, W // 2)
+    return np.concatenate([Y, np.stack([U, V], -1).reshape(H // 2, W)])
+
+
+def _surface(frame, H, W, fmt, pitch, crows):
+    """A decoder-style surface: luma rows of `pitch`, chroma after `crows` rows."""
+    out = np.full((pitch * crows * 3 // 2,), 77, np.uint8)
+    out[:pitch * crows].reshape(crows, pitch)[:H, :W] = frame[:H]
+    if fmt == "NV12":
+        out[pitch * crows:].reshape(crows // 2, pitch)[:H // 2, :W] = frame[H:]
+    else:
+        c = frame[H:].ravel()
+        cp = pitch // 2
+        u = out[pitch * crows:pitch * crows + cp * crows // 2].reshape(crows // 2, cp)
+        v = out[pitch * crows + cp * crows // 2:].reshape(crows // 2, cp)
+        u[:H // 2, :W // 2] = c[:H * W // 4].reshape(H // 2, W // 2)
+        v[:H // 2, :W // 2] = c[H * W // 4:].reshape(H // 2, W // 2)
+    return out
+
+
+@pytest.mark.parametrize("W,H", [(640, 360), (162, 98), (1920, 1080), (6, 2)])
+def test_conversions_match_oracle(gpu_lib, oracle_lib, W, H):
+    N = gpu_lib._native
+    rng = np.random.default_rng(W + H)
+    yuv = rng.integers(0, 256, (3, H * 3 // 2, W), dtype=np.uint8)
+    ref = np.stack([oracle_lib.yuv420_to_bgr(f) for f in yuv])
+    assert np.array_equal(N.yuv420_to_bgr(yuv), ref)
+    nv = np.stack([_nv12(f, H, W) for f in yuv])
+    assert np.array_equal(N.yuv420_to_bgr(nv, "NV12"), ref)
+    bgr = rng.integers(0, 256, (3, H, W, 3), dtype=np.uint8)
+    assert np.array_equal(N.bgr_to_i420(bgr), np.stack([oracle_lib.bgr_to_i420(f) for f in bgr]))
+
+
+@pytest.mark.parametrize("fmt", ["I420", "NV12"])
+def test_conversion_device_pointers_padded_surfaces(gpu_lib, oracle_lib, fmt):
+    import torch
+    N = gpu_lib._native
+    W, H, pitch, crows, n = 322, 180, 384, 192, 4
+    rng = np.random.default_rng(7)
+    yuv = rng.integers(0, 256, (n, H * 3 // 2, W), dtype=np.uint8)
+    src = np.stack([_surface(f if fmt == "I420" else _nv12(f, H, W), H, W, fmt, pitch, crows) for f in yuv])
+    d_src = torch.from_numpy(src).cuda()
+    bp = 3 * W + 12
+    d_out = torch.zeros((n, H, bp), dtype=torch.uint8, device="cuda")
+    N.check(N.lib().dvc_yuv420_to_bgr(d_src.data_ptr(), pitch, N.FORMATS[fmt], crows, W, H, n, src[0].nbytes,
+                                      d_out.data_ptr(), bp, H * bp, 0, None, N.DVC_FLAG_DEVICE_PTRS))
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()[:, :, :3 * W].reshape(n, H, W, 3)
+    assert np.array_equal(got, np.stack([oracle_lib.yuv420_to_bgr(f) for f in yuv]))
+    assert (d_out.cpu().numpy()[:, :, 3 * W:] == 0).all()      # pitch padding untouched
+    # invalid arguments are refused before any launch
+    L = N.lib()
+    assert L.dvc_yuv420_to_bgr(d_src.data_ptr(), pitch, 9, crows, W, H, n, src[0].nbytes, d_out.data_ptr(), bp,
+                               H * bp, 0, None, N.DVC_FLAG_DEVICE_PTRS) != 0
+    assert L.dvc_yuv420_to_bgr(d_src.data_ptr(), pitch, 1, crows, W + 1, H, n, src[0].nbytes, d_out.data_ptr(), bp,
+                               H * bp, 0, None, N.DVC_FLAG_DEVICE_PTRS) != 0
+    assert L.dvc_yuv420_to_bgr(d_src.data_ptr(), pitch, 1, H - 2, W, H, n, src[0].nbytes, d_out.data_ptr(), bp,
+                               H * bp, 0, None, N.DVC_FLAG_DEVICE_PTRS) != 0
+
+
+def _oracle_run(oracle, bgr_frames, W, H, **kw):
+    ref = oracle.OracleFD(W, H, **kw)
+    ref.prime(bgr_frames[0])
+    outs = [ref.step(f)[:2] for f in bgr_frames[1:]]
+    st = ref.stats()
+    ref.close()
+    return outs, st
+
+
+@pytest.mark.parametrize("fmt,W,H,batch", [("I420", 640, 360, 1), ("I420", 642, 362, 5), ("NV12", 640, 360, 4)])
+def test_fd_yuv_input_host(gpu_lib, oracle_lib, fmt, W, H, batch):
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, 9, seed=4)
+    yuv = _i420_frames(oracle_lib, frames)
+    if fmt == "NV12":
+        yuv = np.stack([_nv12(f, H, W) for f in yuv])
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in _i420_frames(oracle_lib, frames)])
+    outs, st = _oracle_run(oracle_lib, bgr, W, H)
+    g = gpu_lib.FDWorker(W, H, device=0, in_format=fmt, max_batch=batch)
+    g.prime(yuv[0])
+    if batch == 1:
+        got = [g.step(f) for f in yuv[1:]]
+    else:
+        ov, cp = g.step_batch(yuv[1:])
+        got = list(zip(ov, cp))
+    for t, ((a, b), (ra, rb)) in enumerate(zip(got, outs)):
+        assert np.array_equal(a, ra), f"overlay differs at frame {t + 1}"
+        assert np.array_equal(b, rb), f"compressed differs at frame {t + 1}"
+    assert g.stats() == st
+    g.close()
+
+
+def test_fd_nv12_device_surfaces_and_resize(gpu_lib, oracle_lib):
+    """Decoder-style NV12 surfaces in HBM (pitch 2048, luma height padded to 1088),
+    device pointers, batches of 3, resized to half size on the GPU (fd:74,91)."""
+    import torch
+    from dvc_amd.synthetic import clip
+    SW, SH, pitch, crows = 1920, 1080, 2048, 1088
+    W, H = SW // 2, SH // 2
+    frames = clip(SW, SH, 7, seed=9)
+    i420 = _i420_frames(oracle_lib, frames)
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    small = np.stack([oracle_lib.resize(f, W, H) for f in bgr])
+    outs, st = _oracle_run(oracle_lib, small, W, H)
+    surf = np.stack([_surface(_nv12(f, SH, SW), SH, SW, "NV12", pitch, crows) for f in i420])
+    d = torch.from_numpy(surf).cuda()
+    ov = torch.empty((6, H, W, 3), dtype=torch.uint8, device="cuda")
+    cp = torch.empty_like(ov)
+    p = gpu_lib.fd.derive_params(W, H, src_width=SW, src_height=SH, in_format="NV12", chroma_rows=crows,
+                                 flags=gpu_lib._native.DVC_FLAG_DEVICE_PTRS)
+    p.max_batch = 3
+    L = gpu_lib._native.lib()
+    h = ctypes.c_void_p()
+    gpu_lib._native.check(L.dvc_fd_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+    try:
+        gpu_lib._native.check(L.dvc_fd_prime(h, d[0].data_ptr(), pitch))
+        gpu_lib._native.check(L.dvc_fd_step_batch(h, d[1].data_ptr(), pitch, surf[0].nbytes, 6, ov.data_ptr(),
+                                                  cp.data_ptr(), 3 * W * H))
+        gpu_lib._native.check(L.dvc_fd_sync(h))
+        s = gpu_lib._native.FdStats()
+        gpu_lib._native.check(L.dvc_fd_get_stats(h, ctypes.byref(s)))
+    finally:
+        L.dvc_fd_destroy(h)
+    ovh, cph = ov.cpu().numpy(), cp.cpu().numpy()
+    for t, (ra, rb) in enumerate(outs):
+        assert np.array_equal(ovh[t], ra), f"overlay differs at frame {t + 1}"
+        assert np.array_equal(cph[t], rb), f"compressed differs at frame {t + 1}"
+    assert {k: int(getattr(s, k)) for k, _ in s._fields_} == st
+
+
+def test_dropin_fd_with_y4m_source(gpu_lib, oracle_lib, tmp_path, monkeypatch):
+    """process_single_video_fd on a Y4M camera file: the 4:2:0 frames go to the
+    worker as is; outputs equal the oracle loop on the converted BGR frames;
+    with DVC_VIDEO_SINK=y4m the outputs are Y4M videos of the BGR2YUV_I420 frames."""
+    from dvc_amd import frame_differencing as fdm
+    from dvc_amd import video_io
+    from dvc_amd.synthetic import clip
+    W, H = 320, 180
+    frames = clip(W, H, 8, seed=11)
+    i420 = _i420_frames(oracle_lib, frames)
+    src = str(tmp_path / "cam3.y4m")
+    with open(src, "wb") as f:
+        f.write(b"YUV4MPEG2 W%d H%d F25:1 Ip A1:1 C420jpeg\n" % (W, H))
+        for fr in i420:
+            f.write(b"FRAME\n" + fr.tobytes())
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    outs, _ = _oracle_run(oracle_lib, bgr, W, H)
+    monkeypatch.setenv("DVC_VIDEO_SINK", "y4m")
+    out_dir = str(tmp_path / "out")
+    fdm.process_single_video_fd(src, out_dir)
+    for name, k in (("dilated_motion_mask_video", 0), ("compressed_final_video", 1)):
+        cap = video_io.open_source(f"{out_dir}/cam3/{name}.y4m")
+        assert cap.isOpened() and cap.get(video_io.CAP_PROP_FRAME_COUNT) == len(outs)
+        assert cap.get(video_io.CAP_PROP_FPS) == 25.0
+        for t in range(len(outs)):
+            ok, f = cap.read_yuv()
+            assert ok and np.array_equal(f, oracle_lib.bgr_to_i420(outs[t][k])), f"{name} frame {t + 1}"
+    txt = open(f"{out_dir}/cam3/execution_times.txt").read()
+    assert f"Frames processed: {len(outs)}" in txt
