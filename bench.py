@@ -57,6 +57,14 @@ PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 rea
 # (+ flow in 8 on the 2nd), write flow 8 on the 1st / the motion bit 1/8 on the 2nd
 OF_FLOW_BYTES_PER_PX = (48.0 + 48.125) / 2
 OF_PIPE_BYTES_PER_PX = 11.25   # SURVEY.md §8d (config 5): frame I/O + state, not Farneback scratch
+# k_flow is not HBM-bound: its work is FarnebackUpdateMatrices (f32) + the box sums
+# and solve (f64) per pixel per iteration (oracle/of_oracle.c oc_update_matrices +
+# oc_update_flow_box_sliding): 81 f32 + 33 f64 flops; an f64 op takes two f32 issue
+# slots on gfx950 (FP64 vector = half the 157.3 TFLOP/s FP32 vector peak), so the
+# VALU roofline counts FP32-equivalent flops against the FP32 vector peak
+OF_FLOW_F32_FLOPS_PER_PX = 81
+OF_FLOW_F64_FLOPS_PER_PX = 33
+FP32_VECTOR_PEAK_TFLOPS = 157.3
 
 
 def pingpong(n: int):
@@ -366,6 +374,23 @@ def main():
             "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
                       "static_blocks": int(vec[4])},
         }
+        if of:   # k_flow's binding axis is the VALU (serial f64 recurrences), not HBM
+            px_it = W * H * per_launch_frames
+            flops = px_it * (OF_FLOW_F32_FLOPS_PER_PX + 2 * OF_FLOW_F64_FLOPS_PER_PX)
+            tf = flops / (avg_ms * 1e-3) / 1e12
+            hbm = line["roofline"]
+            line["roofline"] = {"bound": "valu", "kernel": kname, "achieved": round(tf, 3),
+                                "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s (FP32-equivalent)",
+                                "frac": round(tf / FP32_VECTOR_PEAK_TFLOPS, 4),
+                                "flops_per_launch": int(flops),
+                                "flops_per_px_iteration": {"f32": OF_FLOW_F32_FLOPS_PER_PX,
+                                                           "f64": OF_FLOW_F64_FLOPS_PER_PX},
+                                "traffic": traffic, "frames_per_launch": hbm["frames_per_launch"],
+                                "avg_launch_us": hbm["avg_launch_us"], "launches_timed": kn,
+                                "timed_with": "feed 0 alone",
+                                "hbm": {"achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": hbm["frac"],
+                                        "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"]}}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path, args.cpu_cores)
         print(json.dumps(line), flush=True)

@@ -89,7 +89,7 @@ struct OfBufs {
     // k_flow_scan (sliding box sums): strip hand-off state
     double* scan_g;                // n x strips x h x 5 running sums (sized for the largest level)
     unsigned long long* scan_flags;   // n x strips
-    unsigned int* scan_ctr;        // work-item counter
+    unsigned int* scan_ctr;        // work-item counters (SCAN_Q = 8 queues)
     unsigned int* scan_abort;      // a hand-off wait timed out
 };
 

@@ -617,19 +617,26 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
 //   4. flow = G^-1 h per pixel (or |flow| > thr bits on the finest level's
 //      last iteration).
 // Strips of a frame form a wavefront: strip s waits, block by block, for
-// strip s-1's published state. Items are dequeued in (frame, strip) order from
-// a counter, so the strip an item waits on was taken earlier by a running
-// workgroup: no residency assumption, no deadlock. A wait that ever exceeds
-// ~1 s sets `abort` (reported by the host as an error) instead of hanging.
+// strip s-1's published state. Frames are dealt to SCAN_Q queues, frame t to
+// queue t % SCAN_Q, whose items are dequeued in (frame, strip) order from the
+// queue's counter; workgroup b starts at queue b % SCAN_Q — blocks b, b + 8, ..
+// share an XCD (MI355X_MICROARCH.md § Workgroup dispatch), so a frame's strips
+// and their hand-offs tend to stay in one XCD's L2 — and moves on to the next
+// queues when its own is drained. The strip an item waits on was taken
+// earlier from the same queue by a running workgroup: no residency or
+// placement assumption, no deadlock. A wait that ever exceeds ~1 s sets
+// `abort` (reported by the host as an error) instead of hanging.
 struct ScanArgs {
     FlowArgs f;
     int S;                       // strips across the level
     double* gpub;                // n x S x h x 5: state after each strip's last column, per row
     unsigned long long* flags;   // n x S: (epoch << 32) | row blocks published
-    unsigned int* next;          // work-item counter, zeroed before the launch
+    unsigned int* next;          // SCAN_Q work-item counters, zeroed before the launch
     unsigned int* abort;         // a wait timed out (never in a correct run)
     unsigned int epoch;          // launch number (flags of older launches compare lower)
 };
+
+constexpr int SCAN_Q = 8;   // work queues (XCD groups of workgroups)
 
 // strip width SW (columns) and rows per block RB; LDS: the M ring (RB + 2m + 1
 // rows of SW + 2m + 1 columns x 5 floats) and the block's vertical sums (RB
@@ -773,6 +780,13 @@ __device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long
 
 // SMODE: 0 zero flow, 2 a flow buffer; MM: the largest box radius m served
 // (sizes the per-thread M positions)
+#ifdef DVC_SCAN_STAMPS
+__device__ unsigned long long g_scan_stamps[32 * 96 * 8];
+#define STAMP(k) do { if (tid == 0 && t == 0 && w == A.g.W && s < 32 && yb < 96) \
+    g_scan_stamps[(s * 96 + yb) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
 template <int SW, int RB, int NT, int SMODE, int MM>
 __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, int* s_alive)
 {
@@ -837,7 +851,13 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         }
         __syncthreads();
     }
-    MatPos<MQ> P;   // the next block's M positions, in flight across the block's phases
+    // The pipelined blocks' M positions: P = block b+1 (its R loads in flight
+    // from the start of block b's step, its M written in b's phase 3), Q = block
+    // b+2 (its flow loads in flight across b's step). Every thread issues its
+    // loads unconditionally from valid, clamped positions (wave 0 and positions
+    // past the block are !ok and never stored): a load under a divergent branch
+    // makes hipcc wait for it at the join, which would expose both global
+    // latencies in every step.
     int prow[MQ], pcol[MQ], pidx[MQ];   // this thread's pipelined positions: row in block, column
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
@@ -845,24 +865,28 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         prow[u] = max(pidx[u], 0) / NC;
         pcol[u] = max(pidx[u], 0) - prow[u] * NC;
     }
+    auto set_block = [&](MatPos<MQ>& Q, int yn) {   // positions of the block at row yn + stage 1
+        int nlo, nnpos;
+        block_rows(yn, nlo, nnpos);
+        const int slo = nlo % RING;
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {
+            Q.ok[u] = tid >= 64 && pidx[u] < nnpos;   // nnpos <= RB * NC <= NP * MQ
+            const int r = Q.ok[u] ? nlo + prow[u] : min(nlo, h - 1), sl = slo + (Q.ok[u] ? prow[u] : 0);
+            Q.xs[u] = min(max(CX0 + pcol[u], 0), w - 1);
+            Q.ys[u] = r;
+            Q.off[u] = ((sl >= RING ? sl - RING : sl) * NC + pcol[u]) * 5;
+        }
+        mat_stage1<MQ, SMODE>(A, src, Q);
+    };
+    MatPos<MQ> P, Q;
+    set_block(P, RB);
     const int slot_last = (h - 1) % RING;
     for (int y0 = 0; y0 < h; y0 += RB) {
         const int yb = y0 / RB, nrow = min(RB, h - y0);
-        int nlo, nnpos;
-        block_rows(y0 + RB, nlo, nnpos);
-        const bool pipe = nnpos > 0 && tid >= 64;   // wave-uniform; nnpos <= RB * NC <= NP * MQ
-        if (pipe) {                                 // 1'. the next block's flow loads
-            const int slo = nlo % RING;
-#pragma unroll
-            for (int u = 0; u < MQ; ++u) {
-                P.ok[u] = pidx[u] < nnpos;
-                const int r = P.ok[u] ? nlo + prow[u] : nlo, sl = slo + (P.ok[u] ? prow[u] : 0);
-                P.xs[u] = min(max(CX0 + pcol[u], 0), w - 1);
-                P.ys[u] = r;
-                P.off[u] = ((sl >= RING ? sl - RING : sl) * NC + pcol[u]) * 5;
-            }
-            mat_stage1<MQ, SMODE>(A, src, P);
-        }
+        STAMP(0);
+        mat_stage2<MQ>(A, R0, R1, P);   // 1'. block b+1: R0 and the displaced R1 loads
+        set_block(Q, y0 + 2 * RB);      //     block b+2: positions and flow loads
         // 2. vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
@@ -886,6 +910,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             }
         }
         __syncthreads();   // the M ring is free from here: no reader until the next block's step 2
+        STAMP(1);
         if (tid < 64) {
             // 3. wave 0: the horizontal recurrence, lanes (row i, channel c):
             // g += vsum[x+m] - vsum[x-m-1], from the left strip's published
@@ -894,6 +919,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             // The state after the last column goes to the right neighbour:
             // payload, drain (vmcnt: one wave), flag.
             if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
+            STAMP(2);
             if (tid < nrow * 5) {
                 const int i = tid / 5, c = tid - 5 * i;
                 double* v = sV + i * VS + c;   // column j at v[5 j]
@@ -936,13 +962,14 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-        } else if (pipe) {
-            // 1''. waves 1..: the next block's R0 and displaced R1 loads and M
-            // into the ring, alongside wave 0's chains
-            mat_stage2<MQ>(A, R0, R1, P);
+        } else {
+            // 1''. waves 1..: the next block's M into the ring (its loads were
+            // issued at the start of the step), alongside wave 0's chains
             mat_stage3<MQ>(A, P, sM);
         }
+        STAMP(3);
         __syncthreads();
+        STAMP(4);
         const bool alive = *s_alive;   // uniform: written before the previous barrier
         // 4. flow = G^-1 h per pixel of the block (a wave = one row of 64 columns)
         for (int e = tid; e < RB * SW; e += NT) {
@@ -970,6 +997,16 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             }
         }
         __syncthreads();   // the next block's step 2 overwrites sV
+        STAMP(5);
+#pragma unroll
+        for (int u = 0; u < MQ; ++u) {   // block b+2 becomes the next step's b+1
+            P.ok[u] = Q.ok[u];
+            P.xs[u] = Q.xs[u];
+            P.ys[u] = Q.ys[u];
+            P.off[u] = Q.off[u];
+            P.dx[u] = Q.dx[u];
+            P.dy[u] = Q.dy[u];
+        }
         if (!alive) break;   // an aborted launch drains
     }
 }
@@ -983,17 +1020,21 @@ __global__ void __launch_bounds__(NT, NT == 512 ? 4 : 2) k_flow_scan(ScanArgs S)
     double* sV = lds_s;
     float* sM = reinterpret_cast<float*>(sV + (size_t)RB * scan_vs(SW, m));
     __shared__ int item, alive;
-    const int total = S.S * S.f.n;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            item = (int)atomicAdd(S.next, 1u);
-            alive = 1;
+    const int n = S.f.n;
+    for (int k = 0; k < SCAN_Q; ++k) {
+        const int q = (int)((blockIdx.x + k) % SCAN_Q);
+        const int total = q < n ? ((n - 1 - q) / SCAN_Q + 1) * S.S : 0;   // frames q, q + SCAN_Q, ..
+        for (;;) {
+            if (threadIdx.x == 0) {
+                item = (int)atomicAdd(S.next + q, 1u);
+                alive = 1;
+            }
+            __syncthreads();
+            const int it = item;
+            __syncthreads();
+            if (it >= total) break;
+            scan_strip<SW, RB, NT, SMODE, MM>(S, q + SCAN_Q * (it / S.S), it % S.S, sM, sV, &alive);
         }
-        __syncthreads();
-        const int it = item;
-        __syncthreads();
-        if (it >= total) break;
-        scan_strip<SW, RB, NT, SMODE, MM>(S, it / S.S, it % S.S, sM, sV, &alive);
     }
 }
 
@@ -1528,7 +1569,7 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
-                hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4, s);
+                hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4 * SCAN_Q, s);
                 if (e != hipSuccess) return e;
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
@@ -1585,3 +1626,10 @@ hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, i
 }
 
 }  // namespace dvc
+
+#ifdef DVC_SCAN_STAMPS
+extern "C" int dvc_debug_scan_stamps(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dvc::g_scan_stamps), sizeof(dvc::g_scan_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
