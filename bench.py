@@ -332,8 +332,8 @@ def main():
             kname = "k_flow"
             per_launch_frames = kframes * 2 / max(kn, 1)
             bytes_per_launch = OF_FLOW_BYTES_PER_PX * W * H * per_launch_frames
-            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"), "k_flow", workload,
-                                  per_launch_frames)
+            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"),
+                                  "k_flow" if args.of_direct else "k_flow_scan", workload, per_launch_frames)
         else:
             kname = "k_out"
             per_launch_frames = kframes / max(kn, 1)
