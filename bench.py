@@ -162,7 +162,7 @@ def main():
     ap.add_argument("--of-direct", action="store_true",
                     help="OF: direct per-pixel box sums (DVC_FLAG_OF_DIRECT_SUMS) instead of OpenCV's running sums")
     ap.add_argument("--in-format", choices=("BGR", "I420", "NV12"), default="BGR",
-                    help="FD frames as decoder surfaces: 4:2:0 YUV converted on the GPU in the worker's front "
+                    help="frames as decoder surfaces: 4:2:0 YUV converted on the GPU in the worker's first "
                          "stage (cvtColor YUV2BGR, what VideoCapture.read() returns; video I/O, SURVEY §8f #1)")
     ap.add_argument("--cpu-cores", type=int, default=1,
                     help="CPU baseline: this many feeds on this many host processes (1 = single core)")
@@ -197,7 +197,7 @@ def main():
 
     # per feed: its own synthetic camera (seed = global feed index); frame j of
     # a step is ring frame order[(j + 1) % P] (frame 0 primes the feed)
-    yuv = args.in_format != "BGR" and not of
+    yuv = args.in_format != "BGR"
 
     def to_surface(fr):
         """BGR -> the 4:2:0 surface a decoder would hand over (cvtColor BGR2YUV_I420 on the GPU)."""
@@ -236,8 +236,9 @@ def main():
 
     def make_worker(f, ktiming=False):
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
-        kw = dict(direct_sums=args.of_direct) if of else dict(block_size=args.block_size, kernel_size=args.kernel_size,
-                                release_factor=args.release_factor, in_format=args.in_format)
+        kw = dict(direct_sums=args.of_direct, in_format=args.in_format) if of else \
+            dict(block_size=args.block_size, kernel_size=args.kernel_size, release_factor=args.release_factor,
+                 in_format=args.in_format)
         w = cls(W, H, device=local, device_ptrs=not host_io, ktiming=ktiming, max_batch=batch, **kw)
         w.prime(inputs[f][2])
         return w
@@ -359,7 +360,7 @@ def main():
                        else "frame-differencing (frame_differencing.py)",
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": F,
                        "io": args.io + (" (PCIe-inclusive: frames up, both outputs down)" if host_io else ""),
-                       "ring_frames": R, "noisy": args.noisy, "in_format": "BGR" if of else args.in_format,
+                       "ring_frames": R, "noisy": args.noisy, "in_format": args.in_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),

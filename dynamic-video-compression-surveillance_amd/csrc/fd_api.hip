@@ -191,11 +191,16 @@ struct dvc_fd {
 
 static void free_all(dvc_fd* h)
 {
-    for (Slot& s : h->slot) {
-        void* dev[] = {s.c.mbits, s.c.fbits, s.c.kbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE,
-                       s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin, s.fsrc};
+    for (int k = 0; k < NSLOT; ++k) {
+        Slot& s = h->slot[k];
+        void* dev[] = {s.c.mbits, s.c.kbits, s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin, s.fsrc};
         for (void* p : dev)
             if (p) (void)hipFree(p);
+        if (k == 0) {   // the contour filter's working arrays: one set, shared by the slots
+            void* shared[] = {s.c.fbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE};
+            for (void* p : shared)
+                if (p) (void)hipFree(p);
+        }
         for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_acc, s.ev_out})
             if (e) (void)hipEventDestroy(e);
     }
@@ -444,14 +449,35 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame
-    for (Slot& s : h->slot) {
+    for (int k = 0; k < NSLOT; ++k) {
+        Slot& s = h->slot[k];
         size_t sz[10];
         dvc::CclBufs::sizes(h->g, mb, sz);
         void** ptrs[10] = {(void**)&s.c.mbits, (void**)&s.c.fbits, (void**)&s.c.rs, (void**)&s.c.re,
                            (void**)&s.c.nfg, (void**)&s.c.fpar, (void**)&s.c.gpar, (void**)&s.c.gE,
                            (void**)&s.c.area2, (void**)&s.c.kbits};
-        for (int i = 0; i < 10; ++i)
+        // Only the motion bits (written by the front of a later batch while this
+        // one's contour filter runs) and the kept bits (read by the accumulate
+        // stage after it) belong to a slot; the filter's run index, parents,
+        // areas and filled bits (indices 1..8, ~17 MB per 1080p frame) are
+        // touched only inside the contour-filter stage, whose batches run one
+        // after another on the handle's stream: one set serves all slots.
+        for (int i = 0; i < 10; ++i) {
+            const bool shared = i >= 1 && i <= 8;
+            if (shared && k > 0) continue;   // slot 0's, set below
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
+        }
+        if (k > 0) {
+            const dvc::CclBufs& c0 = h->slot[0].c;
+            s.c.fbits = c0.fbits;
+            s.c.rs = c0.rs;
+            s.c.re = c0.re;
+            s.c.nfg = c0.nfg;
+            s.c.fpar = c0.fpar;
+            s.c.gpar = c0.gpar;
+            s.c.gE = c0.gE;
+            s.c.area2 = c0.area2;
+        }
         if (h->fast) {   // block fields: u16 (B = 4) / u64 (B = 8) per block
             const size_t fb = p.block == 4 ? 2 : 8;
             if ((e = dalloc(&s.dblk, fb * nfield * mb)) != hipSuccess) return bad(e, "hipMalloc");
@@ -532,10 +558,10 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     if ((e = hipMemsetAsync(h->acc, 0, accb, h->stream)) != hipSuccess) return bad(e, "hipMemset");
     // the OUTSIDE gap node of every frame slice is its own root before any
     // k_band runs (its over-budget path may walk through it)
-    for (Slot& s : h->slot) {
+    {
         size_t sz[10];
         dvc::CclBufs::sizes(h->g, mb, sz);
-        if ((e = hipMemsetAsync(s.c.gpar, 0, sz[6], h->stream)) != hipSuccess) return bad(e, "hipMemset");
+        if ((e = hipMemsetAsync(h->slot[0].c.gpar, 0, sz[6], h->stream)) != hipSuccess) return bad(e, "hipMemset");
     }
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return bad(e, "hipStreamSynchronize");
     *out = h;

@@ -17,6 +17,7 @@
 
 #include "../../include/dvc.h"
 #include "host_common.h"
+#include "yuv_kernels.h"
 #include "of_kernels.h"
 
 using dvc_host::fail;
@@ -118,6 +119,8 @@ int vote_threshold(double alpha, int L)
 struct OfSlot {
     hipEvent_t ev_pyr = nullptr, ev_flow = nullptr, ev_mask = nullptr;
     bool recorded = false;
+    uint8_t* fin = nullptr;   // YUV input: the batch's frames converted to BGR (pitch 3W), read by
+                              // the pyramid and by k_of_out
 };
 
 struct dvc_of {
@@ -137,6 +140,7 @@ struct dvc_of {
     dvc::OfBufs b{};
     dvc::DctMat M{};
     int max_batch = 1;
+    int fmt = DVC_FMT_BGR, crows = 0;   // frame format handed to prime/step (DVC_FMT_*)
     long long a_next = 1;
     bool primed = false;
     uint64_t frames = 0;
@@ -216,6 +220,40 @@ static hipError_t of_alloc(dvc_of* h, T** p, size_t bytes)
 
 extern "C" {
 
+// Frames handed to prime/step: BGR rows of `pitch` (>= 3W, % 4), or 4:2:0
+// surfaces (luma pitch >= W; I420: even).
+static bool of_pitch_ok(const dvc_of* h, size_t pitch)
+{
+    const size_t W = h->p.width;
+    if (h->fmt == DVC_FMT_BGR) return pitch >= 3 * W && pitch % 4 == 0;
+    return pitch >= W && (h->fmt != DVC_FMT_I420 || pitch % 2 == 0);
+}
+
+static size_t of_frame_span(const dvc_of* h, size_t pitch)
+{
+    if (h->fmt == DVC_FMT_BGR) return pitch * (h->p.height - 1) + 3 * (size_t)h->p.width;
+    return dvc::yuv_frame_bytes(pitch, h->crows);
+}
+
+// A host frame into pinned staging in the layout the device copy is read with
+// (BGR rows of 3W; YUV: luma rows of W and the chroma plane(s) right after).
+static void of_pack_host(const dvc_of* h, const uint8_t* src, size_t pitch, uint8_t* dst)
+{
+    const size_t W = h->p.width, H = h->p.height;
+    if (h->fmt == DVC_FMT_BGR) {
+        for (size_t y = 0; y < H; ++y) std::memcpy(dst + y * 3 * W, src + y * pitch, 3 * W);
+        return;
+    }
+    const dvc::YuvLayout L = dvc::yuv_layout(src, pitch, h->fmt, h->crows, 0);
+    const dvc::YuvLayout C = dvc::yuv_layout(dst, W, h->fmt, (int)H, 0);
+    for (size_t y = 0; y < H; ++y) std::memcpy(dst + y * W, src + y * pitch, W);
+    const size_t cb = h->fmt == DVC_FMT_NV12 ? W : W / 2;
+    for (size_t y = 0; y < H / 2; ++y) {
+        std::memcpy(dst + C.uoff + y * C.cpitch, src + L.uoff + y * L.cpitch, cb);
+        if (h->fmt == DVC_FMT_I420) std::memcpy(dst + C.voff + y * C.cpitch, src + L.voff + y * L.cpitch, cb);
+    }
+}
+
 int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of** out)
 {
     if (!prm || !out) return fail(DVC_E_INVALID, "NULL argument");
@@ -234,6 +272,10 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     if (p.levels < 0) return fail(DVC_E_INVALID, "levels must be >= 0");
     if (!(p.quant == p.quant) || p.quant == 0.0f) return fail(DVC_E_INVALID, "quant must be nonzero");
     if (p.max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %u outside 1..%d", p.max_batch, DVC_MAX_BATCH);
+    if (p.in_format != DVC_FMT_BGR && p.in_format != DVC_FMT_I420 && p.in_format != DVC_FMT_NV12)
+        return fail(DVC_E_INVALID, "in_format %d unknown", p.in_format);
+    if (p.in_format != DVC_FMT_BGR && p.chroma_rows && (p.chroma_rows < p.height || (p.chroma_rows & 1)))
+        return fail(DVC_E_INVALID, "chroma_rows %d: even and >= the frame height %d", p.chroma_rows, p.height);
     // pyramid depth (oc_fb_levels: min size 32)
     int L = 0;
     {
@@ -249,6 +291,8 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     h->p = p;
     h->device = device;
     h->max_batch = p.max_batch == 0 ? 1 : (int)p.max_batch;
+    h->fmt = p.in_format;
+    h->crows = p.chroma_rows ? p.chroma_rows : p.height;
     const int mb = h->max_batch;
     dvc::OfGeom& g = h->g;
     g.W = p.width;
@@ -398,6 +442,9 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     std::memset(vt, 0, sizeof(vt));
     for (int l = 1; l <= p.window; ++l) vt[l] = (uint8_t)vote_threshold(p.alpha_fraction, l);
     if ((e = hipMemcpy((void*)b.vthr, vt, 256, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+    if (h->fmt != DVC_FMT_BGR)
+        for (OfSlot& sl : h->slot)
+            if ((e = of_alloc(h, &sl.fin, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
     if (!(p.flags & DVC_FLAG_DEVICE_PTRS)) {
         if ((e = of_alloc(h, &h->d_in, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = of_alloc(h, &h->d_mask, N * mb)) != hipSuccess) return bad(e, "hipMalloc");
@@ -415,17 +462,24 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
 int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
 {
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
-    if (pitch < 3 * (size_t)h->p.width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (!of_pitch_ok(h, pitch)) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_sync_all(h));   // no batch of a previous run may still be in flight
     HIP_OK(of_wait_user(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
     const uint8_t* d = bgr;
-    int dp = (int)pitch;
+    int dp = (int)pitch, crows = h->crows;
     if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
-        for (size_t y = 0; y < H; ++y) std::memcpy(h->h_in + y * 3 * W, bgr + y * pitch, 3 * W);
+        of_pack_host(h, bgr, pitch, h->h_in);
         HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, 3 * N, hipMemcpyHostToDevice, h->stream));
         d = h->d_in;
+        dp = (int)(h->fmt == DVC_FMT_BGR ? 3 * W : W);
+        crows = (int)H;
+    }
+    if (h->fmt != DVC_FMT_BGR) {   // cvtColor of the decoded surface (what cap.read() returns, of:54)
+        HIP_OK(dvc::launch_yuv420_to_bgr(dvc::yuv_layout(d, dp, h->fmt, crows, 0), (int)W, (int)H, 1,
+                                         h->slot[0].fin, 3 * W, 3 * N, h->stream));
+        d = h->slot[0].fin;
         dp = (int)(3 * W);
     }
     HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, 3 * N, 0, 1, h->stream));   // of:60
@@ -445,7 +499,7 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
 }  // extern "C"
 
 static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* mask, size_t mstride,
-                      uint8_t* cp, size_t ostride)
+                      uint8_t* cp, size_t ostride, int crows)
 {
     const long long a0 = h->a_next;
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
@@ -454,6 +508,17 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // raw bits flow(i) writes are the evictions only vote(i-2) reads
     OfSlot& S = h->slot[h->seq & 1];
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
+    if (h->fmt != DVC_FMT_BGR) {
+        // 4:2:0 surfaces -> BGR in the slot's frames (of:66,145), read by the
+        // pyramid and by k_of_out: batch i-2's k_of_out must be done with them
+        if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_mask, 0));
+        const size_t W = h->p.width, H = h->p.height;
+        HIP_OK(dvc::launch_yuv420_to_bgr(dvc::yuv_layout(d, dp, h->fmt, crows, fstride), (int)W, (int)H, n, S.fin,
+                                         3 * W, 3 * W * H, h->s_pyr));
+        d = S.fin;
+        dp = (int)(3 * W);
+        fstride = 3 * W * H;
+    }
     HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->s_pyr));
     HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
     HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_pyr, 0));
@@ -503,8 +568,9 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
     if (!h->primed) return fail(DVC_E_STATE, "step before dvc_of_prime");
     if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
     const size_t W = h->p.width, H = h->p.height, N = W * H, row = 3 * W;
-    if (pitch < row || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    if (n > 1 && (fstride < pitch * (H - 1) + row || fstride % 4))
+    const bool yuv = h->fmt != DVC_FMT_BGR;
+    if (!of_pitch_ok(h, pitch)) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
+    if (n > 1 && (fstride < of_frame_span(h, pitch) || (!yuv && fstride % 4)))
         return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
     if (n > 1 && mask && (mstride < N || mstride % 8)) return fail(DVC_E_INVALID, "mask stride %zu invalid", mstride);
     if (n > 1 && compressed && (ostride < 3 * N || ostride % 4))
@@ -518,15 +584,14 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
         uint8_t* mk = mask ? mask + (size_t)f0 * mstride : nullptr;
         uint8_t* cp = compressed ? compressed + (size_t)f0 * ostride : nullptr;
         if (devp) {
-            int rc = of_enqueue(h, in, (int)pitch, fstride, m, mk, mstride, cp, ostride);
+            int rc = of_enqueue(h, in, (int)pitch, fstride, m, mk, mstride, cp, ostride, h->crows);
             if (rc) return rc;
             continue;
         }
-        for (int t = 0; t < m; ++t)
-            for (size_t y = 0; y < H; ++y)
-                std::memcpy(h->h_in + (size_t)t * 3 * N + y * row, in + (size_t)t * fstride + y * pitch, row);
+        for (int t = 0; t < m; ++t) of_pack_host(h, in + (size_t)t * fstride, pitch, h->h_in + (size_t)t * 3 * N);
         HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_pyr));
-        int rc = of_enqueue(h, h->d_in, (int)row, 3 * N, m, mk ? h->d_mask : nullptr, N, cp ? h->d_cp : nullptr, 3 * N);
+        int rc = of_enqueue(h, h->d_in, (int)(yuv ? W : row), 3 * N, m, mk ? h->d_mask : nullptr, N,
+                            cp ? h->d_cp : nullptr, 3 * N, (int)H);
         if (rc) return rc;
         if (mk) HIP_OK(hipMemcpyAsync(h->h_mask, h->d_mask, (size_t)m * N, hipMemcpyDeviceToHost, h->s_mask));
         if (cp) HIP_OK(hipMemcpyAsync(h->h_cp, h->d_cp, (size_t)m * 3 * N, hipMemcpyDeviceToHost, h->s_mask));

@@ -60,8 +60,8 @@ class FDWorker:
         :meth:`prime`/:meth:`step` are ``src_width x src_height`` (the video's,
         default the same) and are resized on the GPU (fd:74,91).
         ``max_batch``: frames one device launch covers in :meth:`step_batch`
-        (the contour-filter scratch is sized for NSLOT = 3 batches of max_batch
-        frames in flight, fd_api.hip). ``stream``: the caller's HIP stream
+        (bit planes for NSLOT = 3 batches of max_batch frames in flight, the
+        contour filter's working arrays for one, fd_api.hip). ``stream``: the caller's HIP stream
         (``torch.cuda.Stream.cuda_stream``), joined as dvc_fd_create documents."""
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
             | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0)

@@ -22,7 +22,8 @@ from . import _native as N
 
 def derive_of_params(width: int, height: int, flow_threshold: float = 0.5, alpha_fraction: float = 0.2,
                      window_size: int = 30, morph_kernel: int = 2, quantization_level: float = 100.0,
-                     flags: int = 0, direct_sums: bool = False) -> N.OfParams:
+                     flags: int = 0, direct_sums: bool = False, in_format: str = "BGR",
+                     chroma_rows: int = 0) -> N.OfParams:
     """dvc_of_params from the reference kwargs of ``temporal_smoothing_flow``
     (of:29-31) and the arguments it hard-codes: Farneback (0.3, 2, 9, 2, 5, 1.1,
     0) at of:72-81, ``QTY_aggressive`` = 100 at of:138. ``direct_sums``: direct
@@ -38,6 +39,8 @@ def derive_of_params(width: int, height: int, flow_threshold: float = 0.5, alpha
     p.morph_kernel = int(morph_kernel)
     p.pyr_scale, p.levels, p.winsize, p.iterations, p.poly_n, p.poly_sigma = 0.3, 2, 9, 2, 5, 1.1
     p.flags = flags
+    p.in_format = N.FORMATS[in_format]
+    p.chroma_rows = int(chroma_rows)
     return p
 
 
@@ -49,6 +52,7 @@ class OFWorker:
         self.params = derive_of_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
+        self.in_format = kwargs.get("in_format", "BGR")
         self.device = int(device)
         self.device_ptrs = device_ptrs
         self._lib = N.lib()
@@ -59,7 +63,16 @@ class OFWorker:
 
     @property
     def _fshape(self):
+        """Input frames: packed BGR, or a (H*3/2, W) 4:2:0 frame."""
+        return (self.H, self.W, 3) if self.in_format == "BGR" else (self.H * 3 // 2, self.W)
+
+    @property
+    def _oshape(self):
         return (self.H, self.W, 3)
+
+    @property
+    def _pitch(self):
+        return 3 * self.W if self.in_format == "BGR" else self.W
 
     def _dev(self, x, name, tail, n=None, batched=False) -> int:
         return B.device_buf(x, tail, self.device, name, n=n, batched=batched)
@@ -67,10 +80,10 @@ class OFWorker:
     def prime(self, frame) -> None:
         """of:54-62: previous gray := gray(frame 0); the vote window is emptied."""
         if self.device_ptrs:
-            N.check(self._lib.dvc_of_prime(self._h, self._dev(frame, "frame", self._fshape)[0], 3 * self.W))
+            N.check(self._lib.dvc_of_prime(self._h, self._dev(frame, "frame", self._fshape)[0], self._pitch))
         else:
             f = B.host_in(frame, self._fshape, "frame")
-            N.check(self._lib.dvc_of_prime(self._h, f.ctypes.data, 3 * self.W))
+            N.check(self._lib.dvc_of_prime(self._h, f.ctypes.data, self._pitch))
 
     def step(self, frame, mask=None, compressed=None, want=("mask", "compressed")):
         """of:70-101 + of:151-183 for one frame. Host mode returns ``(mask,
@@ -79,13 +92,13 @@ class OFWorker:
         if self.device_ptrs:
             addr = self._dev(frame, "frame", self._fshape)[0]
             mk = self._dev(mask, "mask", (self.H, self.W))[0] if mask is not None else None
-            cp = self._dev(compressed, "compressed", self._fshape)[0] if compressed is not None else None
-            N.check(self._lib.dvc_of_step(self._h, addr, 3 * self.W, mk, cp))
+            cp = self._dev(compressed, "compressed", self._oshape)[0] if compressed is not None else None
+            N.check(self._lib.dvc_of_step(self._h, addr, self._pitch, mk, cp))
             return None
         f = B.host_in(frame, self._fshape, "frame")
         mask = B.host_out(mask, (self.H, self.W), "mask", "mask" in want)
-        compressed = B.host_out(compressed, self._fshape, "compressed", "compressed" in want)
-        N.check(self._lib.dvc_of_step(self._h, f.ctypes.data, 3 * self.W,
+        compressed = B.host_out(compressed, self._oshape, "compressed", "compressed" in want)
+        N.check(self._lib.dvc_of_step(self._h, f.ctypes.data, self._pitch,
                                       mask.ctypes.data if mask is not None else None,
                                       compressed.ctypes.data if compressed is not None else None))
         return mask, compressed
@@ -95,23 +108,23 @@ class OFWorker:
         (n, H, W, 3) uint8 in, ``(masks, compressed)`` out. Device mode: CUDA
         tensors on the handle's device or explicit ``(address, n)`` tuples;
         asynchronous, returns None."""
-        fs, ms = 3 * self.W * self.H, self.W * self.H
+        fs, ms, os_ = int(np.prod(self._fshape)), self.W * self.H, 3 * self.W * self.H
         if self.device_ptrs:
             addr, n = self._dev(frames, "frames", self._fshape, batched=True)
             mk = self._dev(mask, "mask", (self.H, self.W), n=n, batched=True)[0] if mask is not None else None
-            cp = self._dev(compressed, "compressed", self._fshape, n=n, batched=True)[0] \
+            cp = self._dev(compressed, "compressed", self._oshape, n=n, batched=True)[0] \
                 if compressed is not None else None
-            N.check(self._lib.dvc_of_step_batch(self._h, addr, 3 * self.W, fs, n, mk, ms, cp, fs))
+            N.check(self._lib.dvc_of_step_batch(self._h, addr, self._pitch, fs, n, mk, ms, cp, os_))
             return None
-        if not isinstance(frames, np.ndarray) or frames.ndim != 4:
-            raise ValueError(f"frames: expected uint8 frames of shape (n, {self.H}, {self.W}, 3)")
+        if not isinstance(frames, np.ndarray) or frames.ndim != len(self._fshape) + 1:
+            raise ValueError(f"frames: expected uint8 frames of shape (n, {', '.join(map(str, self._fshape))})")
         n = int(frames.shape[0])
         f = B.host_in(frames, (n,) + self._fshape, "frames")
         mask = B.host_out(mask, (n, self.H, self.W), "mask", "mask" in want)
-        compressed = B.host_out(compressed, f.shape, "compressed", "compressed" in want)
-        N.check(self._lib.dvc_of_step_batch(self._h, f.ctypes.data, 3 * self.W, fs, n,
+        compressed = B.host_out(compressed, (n,) + self._oshape, "compressed", "compressed" in want)
+        N.check(self._lib.dvc_of_step_batch(self._h, f.ctypes.data, self._pitch, fs, n,
                                             mask.ctypes.data if mask is not None else None, ms,
-                                            compressed.ctypes.data if compressed is not None else None, fs))
+                                            compressed.ctypes.data if compressed is not None else None, os_))
         return mask, compressed
 
     def sync(self) -> None:

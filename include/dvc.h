@@ -143,9 +143,10 @@ typedef struct dvc_fd_params {
     double prime_sigma;
     uint32_t flags;
     uint32_t max_batch; /* 0/1..DVC_MAX_BATCH: frames one device launch covers in
-                           dvc_fd_step_batch (longer calls are chunked). The
-                           per-frame scratch is allocated for three batches in
-                           flight (3 x max_batch frames). */
+                           dvc_fd_step_batch (longer calls are chunked). Bit
+                           planes are allocated for three batches in flight, the
+                           contour filter's working arrays for one (~20 MB per
+                           1080p frame in all; ~8 GB at 383). */
     int32_t src_width;  /* 0: = width  */
     int32_t src_height; /* 0: = height */
     int32_t in_format;  /* DVC_FMT_BGR (0) / DVC_FMT_I420 / DVC_FMT_NV12: the frames
@@ -294,6 +295,9 @@ typedef struct dvc_of_params {
     double poly_sigma;
     uint32_t flags;      /* DVC_FLAG_DEVICE_PTRS | DVC_FLAG_KTIMING | DVC_FLAG_KEEP_PLANES */
     uint32_t max_batch;  /* 0/1..DVC_MAX_BATCH frames per device launch (see dvc_of_step_batch) */
+    int32_t in_format;   /* DVC_FMT_BGR (0) / DVC_FMT_I420 / DVC_FMT_NV12 (of:66,145 read
+                            BGR; 4:2:0 frames are converted on the GPU first) */
+    int32_t chroma_rows; /* YUV: luma rows before the chroma plane(s), 0 = height */
 } dvc_of_params;
 
 typedef struct dvc_of dvc_of;

@@ -421,6 +421,8 @@ class OfParams(ctypes.Structure):
         ("poly_sigma", ctypes.c_double),
         ("flags", ctypes.c_uint32),
         ("max_batch", ctypes.c_uint32),
+        ("in_format", ctypes.c_int32),
+        ("chroma_rows", ctypes.c_int32),
     ]
 
 

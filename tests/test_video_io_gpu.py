@@ -178,3 +178,36 @@ def test_dropin_fd_with_y4m_source(gpu_lib, oracle_lib, tmp_path, monkeypatch):
             assert ok and np.array_equal(f, oracle_lib.bgr_to_i420(outs[t][k])), f"{name} frame {t + 1}"
     txt = open(f"{out_dir}/cam3/execution_times.txt").read()
     assert f"Frames processed: {len(outs)}" in txt
+
+
+@pytest.mark.parametrize("fmt,batch,dev", [("I420", 3, False), ("NV12", 4, True)])
+def test_of_yuv_input(gpu_lib, oracle_lib, fmt, batch, dev):
+    """The OF worker fed 4:2:0 frames (of:66,145 read BGR from VideoCapture):
+    masks and compressed frames equal the oracle worker on the converted frames."""
+    import torch
+    from dvc_amd.synthetic import clip
+    W, H, n = 320, 176, 8
+    frames = clip(W, H, n, seed=6)
+    i420 = _i420_frames(oracle_lib, frames)
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    yuv = i420 if fmt == "I420" else np.stack([_nv12(f, H, W) for f in i420])
+    ref = oracle_lib.OracleOF(W, H)
+    ref.prime(bgr[0])
+    outs = [ref.step(f)[:2] for f in bgr[1:]]
+    ref.close()
+    g = gpu_lib.OFWorker(W, H, device=0, in_format=fmt, max_batch=batch, device_ptrs=dev)
+    if dev:
+        d = torch.from_numpy(yuv).cuda()
+        mk = torch.empty((n - 1, H, W), dtype=torch.uint8, device="cuda")
+        cp = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda")
+        g.prime(d[0])
+        g.step_batch(d[1:], mk, cp)
+        g.sync()
+        mk, cp = mk.cpu().numpy(), cp.cpu().numpy()
+    else:
+        g.prime(yuv[0])
+        mk, cp = g.step_batch(yuv[1:])
+    g.close()
+    for t, (rm, rc) in enumerate(outs):
+        assert np.array_equal(mk[t], rm), f"mask differs at frame {t + 1}"
+        assert np.array_equal(cp[t], rc), f"compressed differs at frame {t + 1}"
