@@ -430,15 +430,18 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->has_user = hip_stream != nullptr || (p.flags & DVC_FLAG_JOIN_STREAM);
     // four internal streams — contour filter, front, accumulate, output —
     // within the default 4 hardware queues (a queue shared by two stages
-    // serialises them); priorities: the latency-bound contour filter and
-    // accumulate chains high, the VALU-bound front low. The caller's stream (if
+    // serialises them); priorities: the HBM-bound output stage (the stream that
+    // is busy the whole period) high, the front low, the latency-bound contour
+    // filter and accumulate chains in between ("lnnh" vs round 1's "lhhn":
+    // +0.1..1 % in interleaved A/Bs with the nontemporal outputs, k_out's
+    // in-pipeline frac 0.38 -> 0.39). The caller's stream (if
     // any) is only joined: each call waits for the work queued on it before the
     // call, and work queued on it after the call waits for the call's outputs.
     int plo = 0, phi = 0;
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
     // priorities of the front, contour-filter, accumulate and output streams:
-    // 'l'ow, 'n'ormal, 'h'igh; DVC_PRIO overrides for sweeps (default "lhhn")
-    static const char* prio = [] { const char* e = getenv("DVC_PRIO"); return e && strlen(e) == 4 ? e : "lhhn"; }();
+    // 'l'ow, 'n'ormal, 'h'igh; DVC_PRIO overrides for sweeps (default "lnnh")
+    static const char* prio = [] { const char* e = getenv("DVC_PRIO"); return e && strlen(e) == 4 ? e : "lnnh"; }();
     auto level = [&](char c) { return c == 'l' ? plo : c == 'h' ? phi : 0; };
     auto mk = [](hipStream_t* st, int pr) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, pr); };
     if ((e = mk(&h->stream, level(prio[1]))) != hipSuccess) return bad(e, "hipStreamCreate");

@@ -33,6 +33,8 @@ from . import _native as N
 from . import video_io
 from .of import OFWorker
 
+READ_AHEAD = int(os.environ.get("DVC_READ_AHEAD", "32"))
+
 
 LOG_FORMAT = "%(asctime)s - %(levelname)s - %(message)s"
 
@@ -88,18 +90,33 @@ def temporal_smoothing_flow(video_path, output_dir, flow_threshold=0.5, alpha_fr
     frame_count = 0
     worker = None
     try:
+        # of:65-101 for READ_AHEAD frames per dvc_of_step_batch call (identical
+        # to one step per frame): the frames are read ahead into page-locked
+        # buffers and the masks come back in one copy per group
+        R = max(1, READ_AHEAD)
         worker = OFWorker(width, height, device=_device(), flow_threshold=flow_threshold,
-                          alpha_fraction=alpha_fraction, window_size=window_size, morph_kernel=morph_kernel)
+                          alpha_fraction=alpha_fraction, window_size=window_size, morph_kernel=morph_kernel,
+                          max_batch=R)
         worker.prime(first_frame)
-        mask = np.empty((height, width), np.uint8)
-        while True:
-            ret, frame = cap.read()
-            if not ret:
+        frames = N.pinned((R, height, width, 3))
+        masks = N.pinned((R, height, width))
+        eof = False
+        while not eof:
+            n = 0
+            while n < R:
+                ret, frame = cap.read()
+                if not ret:
+                    eof = True
+                    break
+                frames[n] = frame
+                n += 1
+            if n == 0:
                 break
-            frame_count += 1
-            worker.step(frame, mask=mask, want=("mask",))
-            out_overlay.write(frame)
-            out_mask.write(mask)
+            worker.step_batch(frames[:n], mask=masks[:n], want=("mask",))
+            for t in range(n):
+                out_overlay.write(frames[t])
+                out_mask.write(masks[t])
+            frame_count += n
     except Exception as e:
         logging.error(f"Error during motion detection: {e}", exc_info=True)
     finally:

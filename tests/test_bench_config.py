@@ -117,7 +117,7 @@ def test_of_bench_config(gpu_lib, oracle_lib):
     import torch
     dvc_amd = gpu_lib
     N = dvc_amd._native
-    W, H, batch, R, stride = 1920, 1080, 16, 64, 61
+    W, H, batch, R, stride = 1920, 1080, 126, 64, 61   # bench.py --path of defaults
     dev = torch.device("cuda", 0)
     ring, idx, seq, first = _sequence(W, H, R, False, seed=0, dev=dev)
     P, passes = seq.shape[0], 2
