@@ -164,6 +164,9 @@ def main():
     ap.add_argument("--in-format", choices=("BGR", "I420", "NV12"), default="BGR",
                     help="frames as decoder surfaces: 4:2:0 YUV converted on the GPU in the worker's first "
                          "stage (cvtColor YUV2BGR, what VideoCapture.read() returns; video I/O, SURVEY §8f #1)")
+    ap.add_argument("--out-format", choices=("BGR", "I420"), default="BGR",
+                    help="FD outputs as the encoder's 4:2:0 input (cvtColor BGR2YUV_I420 of the frames fd:112,131 "
+                         "hand to VideoWriter; DVC_FLAG_OUT_I420) instead of BGR")
     ap.add_argument("--cpu-cores", type=int, default=1,
                     help="CPU baseline: this many feeds on this many host processes (1 = single core)")
     args = ap.parse_args()
@@ -219,19 +222,20 @@ def main():
             ring = [to_surface(fr) for fr in ring]
         fshape = ring[0].shape
         idx = [order[(j + 1) % P] for j in range(P)]
-        oshape = (P, H, W) if of else (P, H, W, 3)     # OF writes a mask plane instead of the red overlay
+        # OF writes a mask plane instead of the red overlay; I420 outputs are (H*3/2, W)
+        oshape = (P, H, W) if of else ((P, H * 3 // 2, W) if args.out_format == "I420" else (P, H, W, 3))
         if args.io == "device":
             seq = torch.empty((P,) + fshape, dtype=torch.uint8, device=dev)
             for j in range(P):
                 seq[j].copy_(torch.from_numpy(ring[idx[j]]))
             outs = (torch.empty(oshape, dtype=torch.uint8, device=dev),
-                    torch.empty((P, H, W, 3), dtype=torch.uint8, device=dev))
+                    torch.empty((P, H, W, 3) if of else oshape[0:1] + oshape[1:], dtype=torch.uint8, device=dev))
         else:
             alloc = dvc_amd._native.pinned if args.io == "host-pinned" else (lambda shp: np.empty(shp, np.uint8))
             seq = alloc((P,) + fshape)
             for j in range(P):
                 seq[j] = ring[idx[j]]
-            outs = (alloc(oshape), alloc((P, H, W, 3)))
+            outs = (alloc(oshape), alloc((P, H, W, 3) if of else oshape))
         first = torch.from_numpy(ring[0]).to(dev) if args.io == "device" else ring[0]
         return seq, outs, first
 
@@ -242,7 +246,7 @@ def main():
         cls = dvc_amd.OFWorker if of else dvc_amd.FDWorker
         kw = dict(direct_sums=args.of_direct, in_format=args.in_format) if of else \
             dict(block_size=args.block_size, kernel_size=args.kernel_size, release_factor=args.release_factor,
-                 in_format=args.in_format)
+                 in_format=args.in_format, out_format=args.out_format)
         w = cls(W, H, device=local, device_ptrs=not host_io, ktiming=ktiming, max_batch=batch, **kw)
         w.prime(inputs[f][2])
         return w
@@ -329,6 +333,8 @@ def main():
             workload += "_per_frame"
         if yuv:
             workload += f"_{args.in_format.lower()}_input"
+        if not of and args.out_format != "BGR":
+            workload += f"_{args.out_format.lower()}_output"
         if of and args.of_direct:
             workload += "_direct_sums"
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
@@ -342,11 +348,16 @@ def main():
         else:
             kname = "k_out"
             per_launch_frames = kframes / max(kn, 1)
-            bytes_per_launch = (BACK_BYTES_PER_PX_FRAME * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
+            # I420 outputs: 1.5 B/px each instead of 3 (k_out still reads the BGR frame)
+            back = BACK_BYTES_PER_PX_FRAME - (3.0 if args.out_format == "I420" else 0.0)
+            bytes_per_launch = (back * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
             traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out", workload,
                                   per_launch_frames)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        pipe = OF_PIPE_BYTES_PER_PX if of else PIPE_BYTES_PER_PX
+        # SURVEY §8d's per-pixel bytes for this configuration: frame in (BGR 3 / 4:2:0
+        # 1.5), state 4, outputs 2 x (BGR 3 / I420 1.5)
+        pipe = OF_PIPE_BYTES_PER_PX if of else (PIPE_BYTES_PER_PX - (1.5 if yuv else 0.0)
+                                                - (3.0 if args.out_format == "I420" else 0.0))
         line = {
             "metric": METRIC if not of else "Mpixels/s (frames/s × H×W) 1080p optical-flow path; % HBM roofline",
             "value": round(value, 2),
@@ -365,6 +376,7 @@ def main():
                        "width": W, "height": H, "frames_per_step": P, "feeds_per_gpu": F,
                        "io": args.io + (" (PCIe-inclusive: frames up, both outputs down)" if host_io else ""),
                        "ring_frames": R, "noisy": args.noisy, "in_format": args.in_format,
+                       "out_format": "mask + BGR" if of else args.out_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),

@@ -17,16 +17,18 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
 SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip", "yuv_kernels.hip"]
-HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h", "yuv_kernels.h"]
+HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h", "yuv_kernels.h", "yuv_px.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 DVC_OK = 0
+DVC_E_INVALID, DVC_E_HIP, DVC_E_STATE, DVC_E_NOMEM, DVC_E_UNSUPPORTED = -1, -2, -3, -4, -5
 DVC_E_ODD_DCT = -6
 DVC_FLAG_DEVICE_PTRS = 0x1
 DVC_FLAG_KTIMING = 0x2
 DVC_FLAG_KEEP_PLANES = 0x4
 DVC_FLAG_JOIN_STREAM = 0x8
 DVC_FLAG_OF_DIRECT_SUMS = 0x10
+DVC_FLAG_OUT_I420 = 0x20
 FMT_BGR, FMT_I420, FMT_NV12 = 0, 1, 2      # DVC_FMT_* frame formats (video I/O)
 FORMATS = {"BGR": FMT_BGR, "I420": FMT_I420, "NV12": FMT_NV12}
 

@@ -158,6 +158,7 @@ struct dvc_fd {
     int crows = 0;          // YUV: luma rows before the chroma planes (device-pointer frames)
     dvc::ResizeTab rt{};
     int B = 4, NBX = 0, NBY = 0, AP = 0;   // block size, blocks (ceil), acc pitch
+    size_t ofb = 0;                        // bytes of one output frame: 3WH (BGR) or 3WH/2 (I420)
     bool fast = true;                      // B = 4, 8: block-field back end
     dvc::GaussTaps kprime{};
     dvc::DctMat M{};
@@ -387,6 +388,10 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         if (p.chroma_rows && (p.chroma_rows < sh || (p.chroma_rows & 1)))
             return fail(DVC_E_INVALID, "chroma_rows %d: even and >= the frame height %d", p.chroma_rows, sh);
     }
+    if ((p.flags & DVC_FLAG_OUT_I420) &&
+        ((p.block != 4 && p.block != 8) || p.width % p.block || p.height % p.block))
+        return fail(DVC_E_UNSUPPORTED, "I420 outputs need block_size 4 or 8 and a frame of whole blocks (%dx%d, b=%d)",
+                    p.width, p.height, p.block);
     const int mb = p.max_batch == 0 ? 1 : (int)p.max_batch;
     if (p.max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %u outside 1..%d", p.max_batch, DVC_MAX_BATCH);
     dvc_fd* h = new dvc_fd();
@@ -404,6 +409,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->sip = 3 * ((h->sw + 3) & ~3);
     h->resize = h->sw != p.width || h->sh != p.height;
     h->fmt = p.in_format;
+    h->ofb = (p.flags & DVC_FLAG_OUT_I420) ? (size_t)p.width * p.height * 3 / 2 : (size_t)p.width * p.height * 3;
     h->crows = p.chroma_rows ? p.chroma_rows : h->sh;
     h->B = p.block;
     h->fast = dvc::fast_block(p.block);
@@ -705,6 +711,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.opitch = 3 * h->p.width;
     a.ostride = ostride;
     a.obytes = (a.opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
+    a.out_i420 = (h->p.flags & DVC_FLAG_OUT_I420) ? 1 : 0;
     a.kbits = S.c.kbits;
     a.dblk = S.dblk;
     a.rblk = S.rblk;
@@ -766,7 +773,7 @@ static int drain_stage(dvc_fd* h, Stage& st)
 {
     if (!st.busy) return DVC_OK;
     HIP_OK(hipEventSynchronize(st.ev_d2h));
-    const size_t N3 = 3 * (size_t)h->p.width * h->p.height;
+    const size_t N3 = h->ofb;
     for (int t = 0; t < st.m; ++t) {
         if (st.ov) std::memcpy(st.ov + (size_t)t * st.ostride, st.h_ov + (size_t)t * N3, N3);
         if (st.cp) std::memcpy(st.cp + (size_t)t * st.ostride, st.h_cp + (size_t)t * N3, N3);
@@ -793,7 +800,7 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
     if (pitch < (yuv ? (size_t)h->sw : srow) || (h->fmt == DVC_FMT_I420 && (pitch & 1)))
         return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
     if (n > 1 && fstride < frame_span(h, pitch, h->crows)) return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
-    if (n > 1 && (overlay || compressed) && ostride < 3 * N)
+    if (n > 1 && (overlay || compressed) && ostride < h->ofb)
         return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(wait_user(h));
@@ -810,9 +817,11 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
         HIP_OK(join_user(h));
         return DVC_OK;
     }
-    const bool pin_in = !yuv && host_pinned(bgr);   // YUV frames are repacked on the host
+    // page-locked frames are DMA'd directly; YUV ones only when already compact
+    // (luma rows of W, chroma right after them), else repacked on the host
+    const bool pin_in = host_pinned(bgr) && (!yuv || (pitch == (size_t)h->sw && h->crows == h->sh));
     const bool pin_out = (!overlay || host_pinned(overlay)) && (!compressed || host_pinned(compressed));
-    const size_t N3 = 3 * N, sfs = (size_t)h->sip * h->sh;
+    const size_t N3 = h->ofb, sfs = (size_t)h->sip * h->sh;
     for (int f0 = 0; f0 < n; f0 += h->max_batch) {
         const int m = std::min(h->max_batch, n - f0);
         Stage& st = h->stage[h->next_stage];
@@ -823,7 +832,12 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
         uint8_t* ov = overlay ? overlay + (size_t)f0 * ostride : nullptr;
         uint8_t* cp = compressed ? compressed + (size_t)f0 * ostride : nullptr;
         HIP_OK(hipStreamWaitEvent(h->s_front, st.ev_free, 0));   // d_in / d_ov / d_cp of two chunks ago are done
-        if (pin_in) {
+        if (pin_in && yuv) {
+            const size_t fb = dvc::yuv_frame_bytes(h->sw, h->sh);
+            for (int t = 0; t < m; ++t)
+                HIP_OK(hipMemcpyAsync(st.d_in + t * sfs, in + (size_t)t * fstride, fb, hipMemcpyHostToDevice,
+                                      h->s_front));
+        } else if (pin_in) {
             for (int t = 0; t < m; ++t)
                 HIP_OK(hipMemcpy2DAsync(st.d_in + t * sfs, h->sip, in + (size_t)t * fstride, pitch, srow, h->sh,
                                         hipMemcpyHostToDevice, h->s_front));

@@ -81,6 +81,7 @@ struct BackArgs {
     int opitch;
     size_t ostride;
     int obytes;             // outputs not 4-byte aligned: byte stores
+    int out_i420;           // outputs are I420 frames (W x H luma + two W/2 x H/2 chroma planes)
     const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
     // fast layout
     void* dblk;             // dilated mask, block-major BxB bit fields per frame (k_dilate -> k_acc)

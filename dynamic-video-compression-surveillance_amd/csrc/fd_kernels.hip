@@ -33,6 +33,7 @@
 
 #include "dvc_device.h"
 #include "fd_kernels.h"
+#include "yuv_px.h"
 
 namespace dvc {
 
@@ -839,6 +840,47 @@ __device__ __forceinline__ void store_row(uint8_t* dst, const uint32_t* w, int b
     }
 }
 
+// One row of a BxB block of an output frame as the encoder's 4:2:0 input
+// (cvtColor BGR2YUV_I420, include/dvc.h DVC_FLAG_OUT_I420): B luma bytes, and
+// on even rows the B/2 chroma samples of the 2x2 quads (their top-left pixel).
+// I420 frame at f: Y plane W x H, then U and V planes of W/2 x H/2.
+template <int B>
+__device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, int x, const uint32_t* w)
+{
+    using namespace yuvpx;
+    uint32_t yv[B], uv[B / 2], vv[B / 2];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+        const int b = (int)((w[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255);
+        const int g = (int)((w[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255);
+        const int r = (int)((w[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255);
+        yv[j] = luma(b, g, r);
+        if (!(j & 1)) {
+            uv[j >> 1] = chroma_u(b, g, r);
+            vv[j >> 1] = chroma_v(b, g, r);
+        }
+    }
+    uint32_t* yo = reinterpret_cast<uint32_t*>(f + (size_t)y * W + x);
+#pragma unroll
+    for (int d = 0; d < B / 4; ++d)
+        __builtin_nontemporal_store(pack4(yv[4 * d], yv[4 * d + 1], yv[4 * d + 2], yv[4 * d + 3]), yo + d);
+    if (!(y & 1)) {
+        const size_t c = (size_t)W * H + (size_t)(y >> 1) * (W >> 1) + (x >> 1), q = (size_t)(W >> 1) * (H >> 1);
+        if constexpr (B == 4) {
+            __builtin_nontemporal_store((uint16_t)(uv[0] | (uv[1] << 8)), reinterpret_cast<uint16_t*>(f + c));
+            __builtin_nontemporal_store((uint16_t)(vv[0] | (vv[1] << 8)), reinterpret_cast<uint16_t*>(f + c + q));
+        } else {
+#pragma unroll
+            for (int d = 0; d < B / 8; ++d) {
+                __builtin_nontemporal_store(pack4(uv[4 * d], uv[4 * d + 1], uv[4 * d + 2], uv[4 * d + 3]),
+                                            reinterpret_cast<uint32_t*>(f + c) + d);
+                __builtin_nontemporal_store(pack4(vv[4 * d], vv[4 * d + 1], vv[4 * d + 2], vv[4 * d + 3]),
+                                            reinterpret_cast<uint32_t*>(f + c + q) + d);
+            }
+        }
+    }
+}
+
 // k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
 // row, one lane per full BxB block, of frame t of the batch.
 template <int B>
@@ -889,7 +931,8 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
                 for (int d = 0; d < 3 * B / 4; ++d)
                     ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
             }
-            store_row<3 * B / 4>(ovf + (size_t)(by + i) * a.opitch + 3 * bx, ow, a.obytes);
+            if (a.out_i420) store_i420_row<B>(ovf, W, H, by + i, bx, ow);
+            else store_row<3 * B / 4>(ovf + (size_t)(by + i) * a.opitch + 3 * bx, ow, a.obytes);
         }
     }
     // compressed (fd:115-130): BGR -> YCrCb; static block: Y' = trunc(clip(IDCT(
@@ -945,7 +988,8 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
         }
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            store_row<3 * B / 4>(cpf + (size_t)(by + i) * a.opitch + 3 * bx, cw[i], a.obytes);
+            if (a.out_i420) store_i420_row<B>(cpf, W, H, by + i, bx, cw[i]);
+            else store_row<3 * B / 4>(cpf + (size_t)(by + i) * a.opitch + 3 * bx, cw[i], a.obytes);
         }
     }
 }

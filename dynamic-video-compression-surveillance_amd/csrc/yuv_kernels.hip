@@ -18,17 +18,13 @@
 #include "../../include/dvc.h"
 #include "host_common.h"
 #include "yuv_kernels.h"
+#include "yuv_px.h"
 
 namespace dvc {
 
 namespace {
 
-constexpr int CY = 1220542, CUB = 2116026, CUG = -409993, CVG = -852492, CVR = 1673527;
-constexpr int CRY = 269484, CGY = 528482, CBY = 102760, CRU = -155188, CGU = -305135, CBU = 460324, CGV = -385875,
-              CBV = -74448;
-constexpr int SHIFT = 20, HALF = 1 << (SHIFT - 1);
-
-__device__ __forceinline__ uint32_t sat8(int v) { return (uint32_t)min(max(v, 0), 255); }
+using namespace yuvpx;
 
 // 4 px of one row sharing chroma samples (u0, v0) for px 0-1 and (u1, v1) for
 // px 2-3 -> 12 BGR bytes as 3 dwords
@@ -43,16 +39,8 @@ __device__ __forceinline__ void yuv4_bgr(uint32_t y4, int u0, int v0, int u1, in
         b[3 * j + 1] = sat8((yy + HALF + CVG * cv + CUG * cu) >> SHIFT);
         b[3 * j + 2] = sat8((yy + HALF + CVR * cv) >> SHIFT);
     }
-    // bytes packed with v_perm: written as shifts and ORs, hipcc (ROCm 7.2)
-    // folds two sat8(x >> 20) into v_ashr_pk_u8_i32, which leaves the upper 16
-    // bits of its destination in place, and the ORs then pick them up (measured:
-    // G and R of every 4th pixel corrupted)
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const uint32_t lo = __builtin_amdgcn_perm(b[4 * d + 1], b[4 * d], 0x0c0c0400u);
-        const uint32_t hi = __builtin_amdgcn_perm(b[4 * d + 3], b[4 * d + 2], 0x0c0c0400u);
-        o[d] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-    }
+    for (int d = 0; d < 3; ++d) o[d] = pack4(b[4 * d], b[4 * d + 1], b[4 * d + 2], b[4 * d + 3]);   // yuv_px.h
 }
 
 template <bool ALIGNED>
@@ -103,10 +91,10 @@ __global__ void __launch_bounds__(256) k_bgr_to_i420(const uint8_t* __restrict__
         uint8_t* yr = f + (size_t)(r + i) * d.ypitch + x;
         for (int j = 0; j < np; ++j) {
             const int b = s[3 * j], g = s[3 * j + 1], rr = s[3 * j + 2];
-            yr[j] = (uint8_t)sat8((CRY * rr + CGY * g + CBY * b + HALF + (16 << SHIFT)) >> SHIFT);
+            yr[j] = (uint8_t)luma(b, g, rr);
             if (i == 0 && !(j & 1)) {
-                us[j >> 1] = (int)sat8((CRU * rr + CGU * g + CBU * b + HALF + (128 << SHIFT)) >> SHIFT);
-                vs[j >> 1] = (int)sat8((CBU * rr + CGV * g + CBV * b + HALF + (128 << SHIFT)) >> SHIFT);
+                us[j >> 1] = (int)chroma_u(b, g, rr);
+                vs[j >> 1] = (int)chroma_v(b, g, rr);
             }
         }
     }

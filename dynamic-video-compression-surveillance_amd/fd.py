@@ -55,16 +55,24 @@ def derive_params(width: int, height: int, block_size: int = 4, motion_threshold
 class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
                  device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
-                 max_batch: int = 1, **kwargs):
+                 max_batch: int = 1, out_format: str = "BGR", **kwargs):
         """``width, height``: the scaled frame size (fd:60-61); frames handed to
         :meth:`prime`/:meth:`step` are ``src_width x src_height`` (the video's,
         default the same) and are resized on the GPU (fd:74,91).
         ``max_batch``: frames one device launch covers in :meth:`step_batch`
         (bit planes for NSLOT = 3 batches of max_batch frames in flight, the
-        contour filter's working arrays for one, fd_api.hip). ``stream``: the caller's HIP stream
-        (``torch.cuda.Stream.cuda_stream``), joined as dvc_fd_create documents."""
+        contour filter's working arrays for one, fd_api.hip). ``stream``: the
+        caller's HIP stream (``torch.cuda.Stream.cuda_stream``), joined as
+        dvc_fd_create documents. ``in_format`` (kwarg) "BGR" / "I420" / "NV12":
+        the frames handed over (4:2:0 decoder surfaces are converted on the GPU);
+        ``out_format`` "BGR" or "I420": overlay and compressed frames as the
+        encoder's 4:2:0 input (DVC_FLAG_OUT_I420)."""
+        if out_format not in ("BGR", "I420"):
+            raise ValueError(f"out_format {out_format!r}: BGR or I420")
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
-            | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0)
+            | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0) \
+            | (N.DVC_FLAG_OUT_I420 if out_format == "I420" else 0)
+        self.out_format = out_format
         self.params = derive_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
         self.W, self.H = int(width), int(height)
@@ -91,8 +99,8 @@ class FDWorker:
 
     @property
     def _oshape(self):
-        """Output frames (scaled size)."""
-        return (self.H, self.W, 3)
+        """Output frames (scaled size): packed BGR, or (H*3/2, W) I420."""
+        return (self.H, self.W, 3) if self.out_format == "BGR" else (self.H * 3 // 2, self.W)
 
     def _dev(self, x, name, n=None, batched=False, tail=None):
         addr, m = B.device_buf(x, tail or self._fshape, self.device, name, n=n, batched=batched)
@@ -141,7 +149,7 @@ class FDWorker:
         handle's device (outputs may hold more frames), or explicit
         ``(address, n)`` tuples of dense frames; asynchronous, returns None.
         """
-        fs, os_ = int(np.prod(self._fshape)), 3 * self.W * self.H
+        fs, os_ = int(np.prod(self._fshape)), int(np.prod(self._oshape))
         if self.device_ptrs:
             addr, n = self._dev(frames, "frames", batched=True)
             ov = self._dev(overlay, "overlay", n=n, batched=True, tail=self._oshape)[0] if overlay is not None else None

@@ -69,6 +69,14 @@ extern "C" {
 #define DVC_FLAG_OF_DIRECT_SUMS 0x10u /* OF: direct per-pixel 9x9 box sums instead
                                      of OpenCV's running sums (the default,
                                      FarnebackUpdateFlow_Blur's order)          */
+#define DVC_FLAG_OUT_I420    0x20u /* FD: overlay and compressed frames are written
+                                     as the encoder's 4:2:0 input instead of BGR:
+                                     cvtColor(frame, COLOR_BGR2YUV_I420) of what
+                                     fd:112 / fd:131 hand to VideoWriter.write —
+                                     I420 frames of W*H*3/2 bytes (Y plane, then
+                                     U and V planes of W/2 x H/2; out_stride >=
+                                     W*H*3/2). block_size 4 or 8, W and H
+                                     multiples of it (else DVC_E_UNSUPPORTED)  */
 
 /* ---- frame formats (video I/O) ----------------------------- */
 /* What the worker's frames are. The reference's are packed BGR straight from

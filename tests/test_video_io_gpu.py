@@ -88,13 +88,21 @@ def _oracle_run(oracle, bgr_frames, W, H, **kw):
     return outs, st
 
 
-@pytest.mark.parametrize("fmt,W,H,batch", [("I420", 640, 360, 1), ("I420", 642, 362, 5), ("NV12", 640, 360, 4)])
-def test_fd_yuv_input_host(gpu_lib, oracle_lib, fmt, W, H, batch):
+@pytest.mark.parametrize("fmt,W,H,batch,pinned", [("I420", 640, 360, 1, False), ("I420", 642, 362, 5, False),
+                                                  ("NV12", 640, 360, 4, False), ("NV12", 640, 360, 4, True),
+                                                  ("I420", 642, 362, 3, True)])
+def test_fd_yuv_input_host(gpu_lib, oracle_lib, fmt, W, H, batch, pinned):
+    """Host 4:2:0 frames: pageable ones repacked through the staging buffers,
+    page-locked compact ones DMA'd directly."""
     from dvc_amd.synthetic import clip
     frames = clip(W, H, 9, seed=4)
     yuv = _i420_frames(oracle_lib, frames)
     if fmt == "NV12":
         yuv = np.stack([_nv12(f, H, W) for f in yuv])
+    if pinned:
+        p = gpu_lib._native.pinned(yuv.shape)
+        p[...] = yuv
+        yuv = p
     bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in _i420_frames(oracle_lib, frames)])
     outs, st = _oracle_run(oracle_lib, bgr, W, H)
     g = gpu_lib.FDWorker(W, H, device=0, in_format=fmt, max_batch=batch)
@@ -211,3 +219,46 @@ def test_of_yuv_input(gpu_lib, oracle_lib, fmt, batch, dev):
     for t, (rm, rc) in enumerate(outs):
         assert np.array_equal(mk[t], rm), f"mask differs at frame {t + 1}"
         assert np.array_equal(cp[t], rc), f"compressed differs at frame {t + 1}"
+
+
+@pytest.mark.parametrize("fmt,block,batch,dev", [("BGR", 4, 5, False), ("NV12", 4, 4, True), ("I420", 8, 3, False)])
+def test_fd_i420_outputs(gpu_lib, oracle_lib, fmt, block, batch, dev):
+    """DVC_FLAG_OUT_I420: overlay and compressed written as the encoder's 4:2:0
+    input = cvtColor(BGR2YUV_I420) of the oracle's BGR outputs (fd:112,131)."""
+    import torch
+    from dvc_amd.synthetic import clip
+    W, H, n = 640, 360, 9
+    frames = clip(W, H, n, seed=12)
+    if fmt == "BGR":
+        src, bgr = frames, frames
+    else:
+        i420 = _i420_frames(oracle_lib, frames)
+        bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+        src = i420 if fmt == "I420" else np.stack([_nv12(f, H, W) for f in i420])
+    kw = dict(block_size=block, kernel_size=10, release_factor=0.3) if block == 8 else {}
+    outs, st = _oracle_run(oracle_lib, bgr, W, H, **kw)
+    g = gpu_lib.FDWorker(W, H, device=0, in_format=fmt, out_format="I420", max_batch=batch, device_ptrs=dev, **kw)
+    if dev:
+        d = torch.from_numpy(np.ascontiguousarray(src)).cuda()
+        ov = torch.empty((n - 1, H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+        cp = torch.empty_like(ov)
+        g.prime(d[0])
+        g.step_batch(d[1:], ov, cp)
+        g.sync()
+        ov, cp = ov.cpu().numpy(), cp.cpu().numpy()
+    else:
+        g.prime(src[0])
+        ov, cp = g.step_batch(np.ascontiguousarray(src[1:]))
+    assert g.stats() == st
+    g.close()
+    for t, (ra, rb) in enumerate(outs):
+        assert np.array_equal(ov[t], oracle_lib.bgr_to_i420(ra)), f"overlay (I420) differs at frame {t + 1}"
+        assert np.array_equal(cp[t], oracle_lib.bgr_to_i420(rb)), f"compressed (I420) differs at frame {t + 1}"
+
+
+def test_fd_i420_outputs_refused_for_partial_blocks(gpu_lib):
+    from dvc_amd._native import DVC_E_UNSUPPORTED, DvcError
+    for W, H, b in [(642, 360, 4), (640, 360, 5), (640, 364, 8)]:
+        with pytest.raises(DvcError) as ei:
+            gpu_lib.FDWorker(W, H, device=0, out_format="I420", block_size=b)
+        assert ei.value.code == DVC_E_UNSUPPORTED
