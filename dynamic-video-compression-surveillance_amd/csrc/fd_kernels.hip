@@ -98,7 +98,7 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 //   5-tap v   packed u16 lanes (sums <= 16 * 4080 < 2^16), (s + 128) >> 8
 //   threshold |cur - prev| > t per u16 lane as bit 15 of d + (0x7fff - t)
 // The previous blurred gray (fd:133) stays in registers as two u16 pairs.
-template <int NW>
+template <int NW, int PF>
 __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
                                                    int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
@@ -162,17 +162,21 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     const int hx = x0 + (hs ? FT_W : -4);
     const uint32_t hoff = (uint32_t)(reflect1(y0 - 2 + min(hr, FT_R - 1), H) * pitch +
                                      3 * (hx >= 0 && hx < W ? hx : xc));
-    uint32_t v0[NR], v1[NR], v2[NR], h0, h1, h2;
-    auto load = [&](const uint8_t* f) {
+    // one frame's quads in registers; PF sets in flight (PF - 1 frames of
+    // prefetch beyond the one being converted)
+    struct Quads { uint32_t v0[NR], v1[NR], v2[NR], h0, h1, h2; };
+    auto load = [&](Quads& qs, const uint8_t* f) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const uint3 q = *reinterpret_cast<const uint3*>(f + off[j]);
-            v0[j] = q.x; v1[j] = q.y; v2[j] = q.z;
+            qs.v0[j] = q.x; qs.v1[j] = q.y; qs.v2[j] = q.z;
         }
         const uint3 q = *reinterpret_cast<const uint3*>(f + hoff);
-        h0 = q.x; h1 = q.y; h2 = q.z;
+        qs.h0 = q.x; qs.h1 = q.y; qs.h2 = q.z;
     };
-    load(bgr + (size_t)t_begin * fstride);
+    Quads qa, qb;
+    load(qa, bgr + (size_t)t_begin * fstride);
+    if constexpr (PF == 2) load(qb, bgr + (size_t)min(t_begin + 1, t_end - 1) * fstride);
 
     // BORDER_REFLECT_101 columns: the halo quad left of x = 0 and px W, W+1
     // (when they lie in this tile's LDS columns) are copies of px 4..1 and
@@ -183,12 +187,13 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     const bool fix_r = iW < 4 * FT_Q;
     constexpr int FB = 64 * ((FT_R + 63) / 64);   // first thread of the right fix-up (after the left one's)
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
-    for (int t = t_begin; t < t_end; ++t) {
+    auto frame = [&](Quads& qs, int t) {
 #pragma unroll
         for (int j = 0; j < NR; ++j)
-            if (NR * NW == FT_R || wave + NW * j < FT_R) sg[wave + NW * j][lane + 1] = gray4_dot(v0[j], v1[j], v2[j]);
+            if (NR * NW == FT_R || wave + NW * j < FT_R)
+                sg[wave + NW * j][lane + 1] = gray4_dot(qs.v0[j], qs.v1[j], qs.v2[j]);
         if (halo_wave) {
-            const uint32_t gh = gray4_dot(h0, h1, h2);
+            const uint32_t gh = gray4_dot(qs.h0, qs.h1, qs.h2);
             if (halo) sg[hr][hs ? FT_Q - 1 : 0] = gh;
         }
         if (fix_l || fix_r) {            // uniform per workgroup
@@ -208,8 +213,9 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
             }
         }
         __syncthreads();
-        // next frame (the last frame reloads itself: an unconditional load)
-        load(bgr + (size_t)min(t + 1, t_end - 1) * fstride);
+        // frame t + PF into the set just converted (the last frames reload
+        // themselves: an unconditional load)
+        load(qs, bgr + (size_t)min(t + PF, t_end - 1) * fstride);
 
 #pragma unroll
         for (int i = 0; i < (FT_R * 64 + NT - 1) / NT; ++i) {
@@ -260,6 +266,14 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
             if ((lane & 7) == 0 && y < H && wi < WW && t >= t_first)
                 reinterpret_cast<uint32_t*>(mb)[((size_t)y * WW + wi) * 2 + ((lane >> 3) & 1)] = w;
         }
+    };
+    if constexpr (PF == 2) {
+        for (int t = t_begin; t < t_end; t += 2) {
+            frame(qa, t);
+            if (t + 1 < t_end) frame(qb, t + 1);   // uniform
+        }
+    } else {
+        for (int t = t_begin; t < t_end; ++t) frame(qa, t);
     }
     // frame n-1's blurred gray becomes the previous gray of the next batch
     if (t_end == n) {
@@ -1309,8 +1323,13 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, int n
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
     static const int xcd = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : 0; }();
-    hipLaunchKernelGGL(k_front<NW>, dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk, gray_in,
-                       gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+    static const int pf = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 1; }();
+    if (pf == 2)
+        hipLaunchKernelGGL((k_front<NW, 2>), dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+    else
+        hipLaunchKernelGGL((k_front<NW, 1>), dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
 }
 
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
