@@ -348,8 +348,9 @@ def main():
         else:
             kname = "k_out"
             per_launch_frames = kframes / max(kn, 1)
-            # I420 outputs: 1.5 B/px each instead of 3 (k_out still reads the BGR frame)
-            back = BACK_BYTES_PER_PX_FRAME - (3.0 if args.out_format == "I420" else 0.0)
+            # I420 outputs: 1.5 B/px each instead of 3; 4:2:0 input surfaces are read
+            # in place (1.5 B/px instead of the BGR frame's 3)
+            back = BACK_BYTES_PER_PX_FRAME - (3.0 if args.out_format == "I420" else 0.0) - (1.5 if yuv else 0.0)
             bytes_per_launch = (back * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
             traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out", workload,
                                   per_launch_frames)

@@ -284,6 +284,17 @@ static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_
            (n <= 1 || fstride % 4 == 0);
 }
 
+// Can k_front / k_out / k_out_gen read these 4:2:0 surfaces in place (no
+// staged BGR copy, fd_kernels.h SrcFmt)? Dword luma rows (pitch % 4 == 0, so
+// rows reach gs bytes), aligned base and stride, no resize in between.
+// DVC_FD_YUV_DIRECT=0 forces the staged conversion (A/B).
+static bool direct_yuv(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
+{
+    static const int on = [] { const char* e = getenv("DVC_FD_YUV_DIRECT"); return e ? atoi(e) : 1; }();
+    return on && h->fmt != DVC_FMT_BGR && !h->resize && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 &&
+           (n <= 1 || fstride % 4 == 0);
+}
+
 static bool host_pinned(const void* p)
 {
     hipPointerAttribute_t a;
@@ -582,10 +593,21 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
 // Frames the kernels read: the caller's in place, or staged into slot S's
 // buffer on s_front (re-pitched, or resized — cv2.resize, fd:74,91). The
 // staged buffer is rewritten only after the slot's previous batch is out.
+// `sf` (nullable: the prime's single frame is always staged as BGR) receives
+// how the kernels read the frames: BGR, or the 4:2:0 surfaces in place.
 static int stage_input(dvc_fd* h, Slot& S, const uint8_t* src, size_t pitch, size_t fstride, int n,
-                       const uint8_t** d, int* dp, size_t* dfs, int crows)
+                       const uint8_t** d, int* dp, size_t* dfs, int crows, dvc::SrcFmt* sf)
 {
+    if (sf) *sf = dvc::SrcFmt{DVC_FMT_BGR, 0, 0, 0};
     if (direct_frames(h, src, pitch, fstride, n)) {
+        *d = src;
+        *dp = (int)pitch;
+        *dfs = fstride;
+        return DVC_OK;
+    }
+    if (sf && direct_yuv(h, src, pitch, fstride, n)) {
+        const dvc::YuvLayout L = dvc::yuv_layout(src, pitch, h->fmt, crows, fstride);
+        *sf = dvc::SrcFmt{h->fmt, L.uoff, L.voff, L.cpitch};
         *d = src;
         *dp = (int)pitch;
         *dfs = fstride;
@@ -650,7 +672,7 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
     const uint8_t* d = nullptr;
     int dp = 0;
     size_t dfs = 0;
-    int rc = stage_input(h, h->slot[0], src, sp, 0, 1, &d, &dp, &dfs, crows);
+    int rc = stage_input(h, h->slot[0], src, sp, 0, 1, &d, &dp, &dfs, crows, nullptr);
     if (rc) return rc;
     HIP_OK(dvc::launch_prime(d, dp, h->gtmp, h->tmp32, h->gray[h->gcur], h->p.width, h->p.height, h->gs, h->kprime,
                              h->s_front));
@@ -687,9 +709,10 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     const uint8_t* d = nullptr;
     int dp = 0;
     size_t dfs = 0;
-    int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs, crows);
+    dvc::SrcFmt sf{};
+    int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs, crows, &sf);
     if (rc) return rc;
-    HIP_OK(dvc::launch_front(d, dp, dfs, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
+    HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
                              h->p.ithresh, h->s_front));
     HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
@@ -704,6 +727,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.bgr = d;
     a.pitch = dp;
     a.fstride = dfs;
+    a.sf = sf;
     a.acc = h->acc;
     a.ap = h->AP;
     a.overlay = ov;

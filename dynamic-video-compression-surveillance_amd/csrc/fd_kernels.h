@@ -61,6 +61,18 @@ struct CclBufs {
     }
 };
 
+// The frames k_front / k_out / k_out_gen read: packed BGR rows (fmt 0,
+// DVC_FMT_BGR), or a decoder's 4:2:0 surfaces read in place (DVC_FMT_I420 /
+// DVC_FMT_NV12, include/dvc.h): luma rows of the frames' pitch, chroma row r
+// at + uoff / voff + r * cpitch (NV12: UV pairs at uoff, voff = uoff + 1),
+// cvtColor YUV2BGR per pixel as the pixels are loaded (fd:87's
+// VideoCapture.read() without a staged BGR copy: 1.5 B/px read instead of 3).
+// In-place reads need pitch % 4 == 0 and a 4-byte aligned base and stride.
+struct SrcFmt {
+    int fmt;
+    size_t uoff, voff, cpitch;
+};
+
 // The back of the loop (dilate, accumulate, overlay, compress). Blocks are
 // B x B (fd:117-118); NBX x NBY of them cover the frame, the last column / row
 // partial when W % B or H % B (fd:120-121). Two layouts:
@@ -74,6 +86,7 @@ struct BackArgs {
     const uint8_t* bgr;   // frame t at bgr + t * fstride, rows of `pitch` bytes (pitch % 4 == 0)
     int pitch;
     size_t fstride;
+    SrcFmt sf;            // BGR, or 4:2:0 surfaces read in place
     uint8_t* acc;         // read before frame 0, written after frame n-1; rows of `ap` bytes
     int ap;
     uint8_t* overlay;     // nullable; frame t at overlay + t * ostride, rows of opitch
@@ -113,7 +126,7 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
                         int W, int H, int gs, const GaussTaps& k, hipStream_t s);
 // frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
 // gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW
-hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n, const uint8_t* gray_in,
                         uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
 // cv2.resize(frame, (W, H)) INTER_LINEAR 8UC3 (fd:74,91) of n frames into dst
 // (rows of dpitch, frames of dstride). Tables from resize_tables().

@@ -34,6 +34,7 @@
 #include "dvc_device.h"
 #include "fd_kernels.h"
 #include "yuv_px.h"
+#include "../../include/dvc.h"
 
 namespace dvc {
 
@@ -98,9 +99,32 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 //   5-tap v   packed u16 lanes (sums <= 16 * 4080 < 2^16), (s + 128) >> 8
 //   threshold |cur - prev| > t per u16 lane as bit 15 of d + (0x7fff - t)
 // The previous blurred gray (fd:133) stays in registers as two u16 pairs.
-template <int NW, int PF>
-__global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, int n,
-                                                   int chunk, const uint8_t* __restrict__ gray_in,
+// A 4-px quad (x even) of a 4:2:0 surface as loaded (y4 = its luma dword;
+// I420: c1 / c2 = the u16 of U / V samples; NV12: c1 = the dword U0 V0 U1 V1)
+// -> 12 packed BGR bytes (cvtColor YUV2BGR, yuv_px.h)
+template <int FMT>
+__device__ __forceinline__ void quad_bgr(uint32_t y4, uint32_t c1, uint32_t c2, uint32_t o[3])
+{
+    if constexpr (FMT == DVC_FMT_NV12) yuvpx::yuv4_bgr(y4, c1 & 255, (c1 >> 8) & 255, (c1 >> 16) & 255, c1 >> 24, o);
+    else yuvpx::yuv4_bgr(y4, c1 & 255, c2 & 255, (c1 >> 8) & 255, (c2 >> 8) & 255, o);
+}
+
+// gray of a loaded quad: 12 BGR bytes (v0..v2), or a 4:2:0 quad via quad_bgr
+template <int FMT>
+__device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t v2)
+{
+    if constexpr (FMT == DVC_FMT_BGR) {
+        return gray4_dot(v0, v1, v2);
+    } else {
+        uint32_t o[3];
+        quad_bgr<FMT>(v0, v1, v2, o);
+        return gray4_dot(o[0], o[1], o[2]);
+    }
+}
+
+template <int NW, int PF, int FMT>
+__global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+                                                   int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands)
 {
@@ -150,29 +174,51 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     // l (12 contiguous bytes); rows past FT_R (NW > 4) reload a valid row and
     // are dropped. The 2 x FT_R halo quads left / right of the tile are loaded
     // and converted once, by threads 0 .. 2*FT_R-1 (thread 2r + side).
-    // Addresses are a uniform frame base + 32-bit per-lane offsets.
+    // Addresses are a uniform frame base + 32-bit per-lane offsets. A 4:2:0
+    // surface (FMT != BGR): the quad's luma dword and its chroma (I420: a u16
+    // of U and one of V, dv bytes apart; NV12: one UVUV dword) instead.
+    constexpr bool YUV = FMT != DVC_FMT_BGR;
     constexpr int NR = (FT_R + NW - 1) / NW;
-    uint32_t off[NR];
+    uint32_t off[NR], coff[NR];
+    auto row_off = [&](int y, int xq, uint32_t& o, uint32_t& co) {
+        if constexpr (YUV) {
+            o = (uint32_t)(y * pitch + xq);
+            co = (uint32_t)(sf.uoff + (size_t)(y >> 1) * sf.cpitch + (FMT == DVC_FMT_NV12 ? xq : xq >> 1));
+        } else {
+            o = (uint32_t)(y * pitch + 3 * xq);
+            co = 0;
+        }
+    };
 #pragma unroll
-    for (int j = 0; j < NR; ++j)
-        off[j] = (uint32_t)(reflect1(y0 - 2 + min(wave + NW * j, FT_R - 1), H) * pitch + 3 * xc);
+    for (int j = 0; j < NR; ++j) row_off(reflect1(y0 - 2 + min(wave + NW * j, FT_R - 1), H), xc, off[j], coff[j]);
+    const uint32_t dv = (uint32_t)(sf.voff - sf.uoff);
     const bool halo_wave = __builtin_amdgcn_readfirstlane(wave) < (2 * FT_R + 63) / 64;   // scalar branch
     const bool halo = halo_wave && tid < 2 * FT_R;
     const int hr = min(tid >> 1, FT_R - 1), hs = tid & 1;
     const int hx = x0 + (hs ? FT_W : -4);
-    const uint32_t hoff = (uint32_t)(reflect1(y0 - 2 + min(hr, FT_R - 1), H) * pitch +
-                                     3 * (hx >= 0 && hx < W ? hx : xc));
+    uint32_t hoff, hcoff;
+    row_off(reflect1(y0 - 2 + min(hr, FT_R - 1), H), hx >= 0 && hx < W ? hx : xc, hoff, hcoff);
     // one frame's quads in registers; PF sets in flight (PF - 1 frames of
     // prefetch beyond the one being converted)
     struct Quads { uint32_t v0[NR], v1[NR], v2[NR], h0, h1, h2; };
+    auto load_quad = [&](const uint8_t* f, uint32_t o, uint32_t co, uint32_t& a, uint32_t& b, uint32_t& c) {
+        if constexpr (FMT == DVC_FMT_BGR) {
+            const uint3 q = *reinterpret_cast<const uint3*>(f + o);
+            a = q.x; b = q.y; c = q.z;
+        } else if constexpr (FMT == DVC_FMT_NV12) {
+            a = *reinterpret_cast<const uint32_t*>(f + o);
+            b = *reinterpret_cast<const uint32_t*>(f + co);
+            c = 0;
+        } else {
+            a = *reinterpret_cast<const uint32_t*>(f + o);
+            b = *reinterpret_cast<const uint16_t*>(f + co);
+            c = *reinterpret_cast<const uint16_t*>(f + co + dv);
+        }
+    };
     auto load = [&](Quads& qs, const uint8_t* f) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            const uint3 q = *reinterpret_cast<const uint3*>(f + off[j]);
-            qs.v0[j] = q.x; qs.v1[j] = q.y; qs.v2[j] = q.z;
-        }
-        const uint3 q = *reinterpret_cast<const uint3*>(f + hoff);
-        qs.h0 = q.x; qs.h1 = q.y; qs.h2 = q.z;
+        for (int j = 0; j < NR; ++j) load_quad(f, off[j], coff[j], qs.v0[j], qs.v1[j], qs.v2[j]);
+        load_quad(f, hoff, hcoff, qs.h0, qs.h1, qs.h2);
     };
     Quads qa, qb;
     load(qa, bgr + (size_t)t_begin * fstride);
@@ -191,9 +237,9 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
 #pragma unroll
         for (int j = 0; j < NR; ++j)
             if (NR * NW == FT_R || wave + NW * j < FT_R)
-                sg[wave + NW * j][lane + 1] = gray4_dot(qs.v0[j], qs.v1[j], qs.v2[j]);
+                sg[wave + NW * j][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
         if (halo_wave) {
-            const uint32_t gh = gray4_dot(qs.h0, qs.h1, qs.h2);
+            const uint32_t gh = quad_gray<FMT>(qs.h0, qs.h1, qs.h2);
             if (halo) sg[hr][hs ? FT_Q - 1 : 0] = gh;
         }
         if (fix_l || fix_r) {            // uniform per workgroup
@@ -896,8 +942,10 @@ __device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, 
 }
 
 // k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
-// row, one lane per full BxB block, of frame t of the batch.
-template <int B>
+// row, one lane per full BxB block, of frame t of the batch. FMT != BGR: the
+// block's pixels from a 4:2:0 surface (B luma bytes per row, the chroma row of
+// each row pair loaded once), converted to packed BGR in registers.
+template <int B, int FMT>
 __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int ty, int lane, int wave)
 {
     const int W = a.g.W, H = a.g.H;
@@ -905,11 +953,35 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
     if (bx + B > W || by + B > H) return;   // partial edge blocks: k_out_gen
     const uint8_t* f = a.bgr + (size_t)t * a.fstride;
     uint32_t px[B][3 * B / 4];
+    if constexpr (FMT == DVC_FMT_BGR) {
 #pragma unroll
-    for (int i = 0; i < B; ++i) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * a.pitch + 3 * bx);
+        for (int i = 0; i < B; ++i) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * a.pitch + 3 * bx);
 #pragma unroll
-        for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
+            for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < B; i += 2) {
+            const uint8_t* cr = f + a.sf.uoff + (size_t)((by + i) >> 1) * a.sf.cpitch + (FMT == DVC_FMT_NV12 ? bx : bx / 2);
+            uint32_t c1[B / 4], c2[B / 4];
+#pragma unroll
+            for (int d = 0; d < B / 4; ++d) {
+                if constexpr (FMT == DVC_FMT_NV12) {
+                    c1[d] = reinterpret_cast<const uint32_t*>(cr)[d];
+                    c2[d] = 0;
+                } else {
+                    c1[d] = reinterpret_cast<const uint16_t*>(cr)[d];
+                    c2[d] = reinterpret_cast<const uint16_t*>(cr + (a.sf.voff - a.sf.uoff))[d];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t* yr = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i + k) * a.pitch + bx);
+#pragma unroll
+                for (int d = 0; d < B / 4; ++d) quad_bgr<FMT>(yr[d], c1[d], c2[d], &px[i + k][3 * d]);
+            }
+        }
     }
     const bool is_static =
         (a.sbits[(size_t)t * a.sstride + (size_t)(by / B) * a.SW + (bx / B >> 6)] >> ((bx / B) & 63)) & 1ull;
@@ -1011,14 +1083,14 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
 // Grid-stride over the batch's (frame, tile) pairs with a bounded grid: a few
 // long-lived workgroups per CU keep HBM saturated while leaving wave slots to
 // the latency-bound contour-filter kernels running beside it on other streams.
-template <int B>
+template <int B, int FMT>
 __global__ void __launch_bounds__(256) k_out(BackArgs a, int ntx, int nty)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int per = ntx * nty, total = per * a.n;
     for (int u = blockIdx.x; u < total; u += gridDim.x) {   // no barrier in the loop
         const int t = u / per, r = u - t * per, ty = r / ntx;
-        out_tile<B>(a, t, r - ty * ntx, ty, lane, wave);
+        out_tile<B, FMT>(a, t, r - ty * ntx, ty, lane, wave);
     }
 }
 
@@ -1205,8 +1277,16 @@ __global__ void __launch_bounds__(256) k_out_gen(BackArgs a, GenRegion R, int fa
     for (int e = tid; e < npx; e += 256) {
         const int i = e / JW, j = e - i * JW, y = py0 + i, x = px0 + j;
         const int b = (i / B) * nbx + j / B;
-        const uint8_t* px = f + (size_t)y * a.pitch + 3 * x;
-        const int cb = px[0], cg = px[1], cr = px[2];
+        int cb, cg, cr;
+        if (a.sf.fmt == DVC_FMT_BGR) {
+            const uint8_t* px = f + (size_t)y * a.pitch + 3 * x;
+            cb = px[0];
+            cg = px[1];
+            cr = px[2];
+        } else {   // a 4:2:0 surface read in place
+            const size_t c = (size_t)(y >> 1) * a.sf.cpitch + (a.sf.fmt == DVC_FMT_NV12 ? (x & ~1) : (x >> 1));
+            yuvpx::yuv_px_bgr(f[(size_t)y * a.pitch + x], f[a.sf.uoff + c], f[a.sf.voff + c], cb, cg, cr);
+        }
         if (a.overlay) {
             bool red;
             if (fast) {
@@ -1307,8 +1387,9 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
 }
 
 template <int NW>
-static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
-                            uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
+static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n,
+                            const uint8_t* gray_in, uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g,
+                            int ithresh, hipStream_t s)
 {
     constexpr int FT_H = 4 * NW;
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
@@ -1324,22 +1405,29 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, int n
     chunks = (n + chunk - 1) / chunk;
     static const int xcd = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : 0; }();
     static const int pf = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 1; }();
-    if (pf == 2)
-        hipLaunchKernelGGL((k_front<NW, 2>), dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk,
+    const dim3 grid(tx, ty, chunks), block(64 * NW);
+    if (sf.fmt == DVC_FMT_I420)
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+    else if (sf.fmt == DVC_FMT_NV12)
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+    else if (pf == 2)
+        hipLaunchKernelGGL((k_front<NW, 2, DVC_FMT_BGR>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
     else
-        hipLaunchKernelGGL((k_front<NW, 1>), dim3(tx, ty, chunks), dim3(64 * NW), 0, s, bgr, pitch, fstride, n, chunk,
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
 }
 
-hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, int n, const uint8_t* gray_in,
+hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n, const uint8_t* gray_in,
                         uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
 {
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
-    if (nw == 16) launch_front_nw<16>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
-    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
-    else launch_front_nw<4>(bgr, pitch, fstride, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    if (nw == 16) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
     return hipGetLastError();
 }
 
@@ -1469,8 +1557,13 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s)
     }();
     const int ntx = (a.g.W + 64 * B - 1) / (64 * B), nty = (a.g.H + 4 * B - 1) / (4 * B);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
-    if (B == 4) hipLaunchKernelGGL(k_out<4>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else hipLaunchKernelGGL(k_out<8>, dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    const int f = a.sf.fmt;
+    if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4) hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<8, DVC_FMT_I420>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<8, DVC_FMT_NV12>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     return hipGetLastError();
 }
 

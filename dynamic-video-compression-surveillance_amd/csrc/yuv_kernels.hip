@@ -26,23 +26,6 @@ namespace {
 
 using namespace yuvpx;
 
-// 4 px of one row sharing chroma samples (u0, v0) for px 0-1 and (u1, v1) for
-// px 2-3 -> 12 BGR bytes as 3 dwords
-__device__ __forceinline__ void yuv4_bgr(uint32_t y4, int u0, int v0, int u1, int v1, uint32_t o[3])
-{
-    uint32_t b[12];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int cu = (j < 2 ? u0 : u1) - 128, cv = (j < 2 ? v0 : v1) - 128;
-        const int yy = max((int)((y4 >> (8 * j)) & 255) - 16, 0) * CY;
-        b[3 * j + 0] = sat8((yy + HALF + CUB * cu) >> SHIFT);
-        b[3 * j + 1] = sat8((yy + HALF + CVG * cv + CUG * cu) >> SHIFT);
-        b[3 * j + 2] = sat8((yy + HALF + CVR * cv) >> SHIFT);
-    }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) o[d] = pack4(b[4 * d], b[4 * d + 1], b[4 * d + 2], b[4 * d + 3]);   // yuv_px.h
-}
-
 template <bool ALIGNED>
 __global__ void __launch_bounds__(256) k_yuv420_to_bgr(YuvLayout s, int W, int H, uint8_t* __restrict__ dst,
                                                        size_t dpitch, size_t dstride)

@@ -1,6 +1,7 @@
 // yuv_px.h — per-pixel BT.601 conversions shared by the video-I/O kernels
-// (yuv_kernels.hip) and the FD output stage writing encoder-ready I420
-// (fd_kernels.hip k_out): OpenCV 4.11 cvtColor's fixed point
+// (yuv_kernels.hip) and the FD kernels reading decoder surfaces in place
+// (k_front, k_out, k_out_gen) and writing encoder-ready I420 (k_out):
+// OpenCV 4.11 cvtColor's fixed point
 // (color_yuv.simd.hpp; restated in oracle/yuv_oracle.c). Internal.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -39,6 +40,32 @@ __device__ __forceinline__ uint32_t pack4(uint32_t b0, uint32_t b1, uint32_t b2,
     const uint32_t lo = __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u);
     const uint32_t hi = __builtin_amdgcn_perm(b3, b2, 0x0c0c0400u);
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// YUV2BGR_I420 / _NV12 of one pixel: Y and its 2x2 quad's (u, v)
+__device__ __forceinline__ void yuv_px_bgr(int y, int u, int v, int& b, int& g, int& r)
+{
+    const int cu = u - 128, cv = v - 128, yy = max(y - 16, 0) * CY;
+    b = (int)sat8((yy + HALF + CUB * cu) >> SHIFT);
+    g = (int)sat8((yy + HALF + CVG * cv + CUG * cu) >> SHIFT);
+    r = (int)sat8((yy + HALF + CVR * cv) >> SHIFT);
+}
+
+// 4 px of one row (x even) sharing chroma samples (u0, v0) for px 0-1 and
+// (u1, v1) for px 2-3 -> 12 packed BGR bytes as 3 dwords
+__device__ __forceinline__ void yuv4_bgr(uint32_t y4, int u0, int v0, int u1, int v1, uint32_t o[3])
+{
+    uint32_t p[12];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int b, g, r;
+        yuv_px_bgr((int)((y4 >> (8 * j)) & 255), j < 2 ? u0 : u1, j < 2 ? v0 : v1, b, g, r);
+        p[3 * j] = (uint32_t)b;
+        p[3 * j + 1] = (uint32_t)g;
+        p[3 * j + 2] = (uint32_t)r;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) o[d] = pack4(p[4 * d], p[4 * d + 1], p[4 * d + 2], p[4 * d + 3]);
 }
 
 }  // namespace yuvpx

@@ -157,6 +157,50 @@ def test_fd_nv12_device_surfaces_and_resize(gpu_lib, oracle_lib):
     assert {k: int(getattr(s, k)) for k, _ in s._fields_} == st
 
 
+@pytest.mark.parametrize("fmt,W,H,pitch,crows,block,batch", [
+    ("I420", 1920, 1080, 2048, 1088, 4, 3),   # decoder surface, fast blocks, 2 launches + a partial one
+    ("NV12", 642, 362, 704, 368, 4, 4),       # W % 4 = 2, H % 4 = 2: partial edge blocks via k_out_gen
+    ("I420", 640, 360, 640, 360, 6, 3),       # generic block size: k_out_gen only
+    ("NV12", 646, 360, 648, 360, 8, 8),       # B = 8, right edge blocks 6 px wide
+])
+def test_fd_yuv_surfaces_read_in_place(gpu_lib, oracle_lib, fmt, W, H, pitch, crows, block, batch):
+    """4:2:0 surfaces in HBM with pitch % 4 == 0 and no resize are read in place
+    by k_front / k_out / k_out_gen (cvtColor per pixel as loaded, no staged BGR
+    frames): outputs and stats equal the oracle on the converted frames."""
+    import torch
+    from dvc_amd.synthetic import clip
+    n = 8
+    frames = clip(W, H, n, seed=21)
+    i420 = _i420_frames(oracle_lib, frames)
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    kw = dict(block_size=block)
+    outs, st = _oracle_run(oracle_lib, bgr, W, H, **kw)
+    surf = np.stack([_surface(f if fmt == "I420" else _nv12(f, H, W), H, W, fmt, pitch, crows) for f in i420])
+    d = torch.from_numpy(surf).cuda()
+    ov = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda")
+    cp = torch.empty_like(ov)
+    p = gpu_lib.fd.derive_params(W, H, in_format=fmt, chroma_rows=crows, flags=gpu_lib._native.DVC_FLAG_DEVICE_PTRS,
+                                 **kw)
+    p.max_batch = batch
+    L = gpu_lib._native.lib()
+    h = ctypes.c_void_p()
+    gpu_lib._native.check(L.dvc_fd_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+    try:
+        gpu_lib._native.check(L.dvc_fd_prime(h, d[0].data_ptr(), pitch))
+        gpu_lib._native.check(L.dvc_fd_step_batch(h, d[1].data_ptr(), pitch, surf[0].nbytes, n - 1, ov.data_ptr(),
+                                                  cp.data_ptr(), 3 * W * H))
+        gpu_lib._native.check(L.dvc_fd_sync(h))
+        s = gpu_lib._native.FdStats()
+        gpu_lib._native.check(L.dvc_fd_get_stats(h, ctypes.byref(s)))
+    finally:
+        L.dvc_fd_destroy(h)
+    ovh, cph = ov.cpu().numpy(), cp.cpu().numpy()
+    for t, (ra, rb) in enumerate(outs):
+        assert np.array_equal(ovh[t], ra), f"overlay differs at frame {t + 1}"
+        assert np.array_equal(cph[t], rb), f"compressed differs at frame {t + 1}"
+    assert {k: int(getattr(s, k)) for k, _ in s._fields_} == st
+
+
 def test_dropin_fd_with_y4m_source(gpu_lib, oracle_lib, tmp_path, monkeypatch):
     """process_single_video_fd on a Y4M camera file: the 4:2:0 frames go to the
     worker as is; outputs equal the oracle loop on the converted BGR frames;
