@@ -180,11 +180,18 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DVC_BENCH_ONE_DEVICE=1: rehearse the N > 1 flow on a one-GPU box (every
+    # rank on cuda:0, gloo for the end-of-run reduction; RCCL refuses two ranks
+    # on one device). The driver's multi-GPU runs never set it.
+    one_dev = os.environ.get("DVC_BENCH_ONE_DEVICE") == "1"
+    local = 0 if one_dev else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     W, H = args.width, args.height
     of = args.path == "of"
@@ -313,7 +320,7 @@ def main():
     kframes = ksteps * P
 
     vec = torch.tensor([elapsed, st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
-                       dtype=torch.float64, device=dev)
+                       dtype=torch.float64, device="cpu" if one_dev else dev)
     if world > 1:
         tmax = vec[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
