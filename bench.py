@@ -134,6 +134,27 @@ def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path
                       f"synthetic workload (seeds 0..{len(jobs) - 1}), {nf} frames in {secs:.1f} s"}
 
 
+def copy_bandwidth(dev, nbytes=1 << 30, reps=10):
+    """This GPU's device-to-device copy rate in GB/s (bytes read + written), the
+    practical ceiling SURVEY.md §8d asks the roofline to be quoted against
+    beside the 8 TB/s spec: one 1 GiB buffer copied `reps` times, event-timed."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -338,6 +359,8 @@ def main():
             workload += f"_{args.io}_io"
         if args.per_frame:
             workload += "_per_frame"
+        if args.noisy:
+            workload += "_noisy"
         if yuv:
             workload += f"_{args.in_format.lower()}_input"
         if not of and args.out_format != "BGR":
@@ -399,6 +422,10 @@ def main():
             "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
                       "static_blocks": int(vec[4])},
         }
+        # the same kernel's bytes (and the pipeline's) against this box's measured copy rate
+        cp_gbs = copy_bandwidth(dev)
+        line["roofline"]["copy"] = {"GBps": round(cp_gbs, 1), "frac": round(achieved / cp_gbs, 4),
+                                    "pipeline_frac": round(line["config"]["pipeline_GBps_per_gpu"] / cp_gbs, 4)}
         if of:   # k_flow's binding axis is the VALU (serial f64 recurrences), not HBM
             px_it = W * H * per_launch_frames
             flops = px_it * (OF_FLOW_F32_FLOPS_PER_PX + 2 * OF_FLOW_F64_FLOPS_PER_PX)
@@ -414,7 +441,7 @@ def main():
                                 "avg_launch_us": hbm["avg_launch_us"], "launches_timed": kn,
                                 "timed_with": "feed 0 alone",
                                 "hbm": {"achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": hbm["frac"],
+                                        "frac": hbm["frac"], "copy": hbm.get("copy"),
                                         "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"]}}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path, args.cpu_cores)
