@@ -113,6 +113,7 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 struct Slot {
     dvc::CclBufs c{};
     uint64_t *dblk = nullptr, *rblk = nullptr, *sbits = nullptr;    // fast back end (B = 4, 8)
+    uint8_t* docc = nullptr;   // fast back end: block rows with dilated bits (BackArgs::docc)
     uint64_t *dbits = nullptr, *rbits = nullptr, *zbits = nullptr;  // generic back end (row-major planes)
     uint8_t* fin = nullptr;    // resized / re-pitched / converted input frames (pitch ip), allocated when needed
     uint8_t* fsrc = nullptr;   // YUV frames converted to BGR at the source size, before the resize (pitch sip)
@@ -194,7 +195,8 @@ static void free_all(dvc_fd* h)
 {
     for (int k = 0; k < NSLOT; ++k) {
         Slot& s = h->slot[k];
-        void* dev[] = {s.c.mbits, s.c.kbits, s.dblk, s.rblk, s.sbits, s.dbits, s.rbits, s.zbits, s.fin, s.fsrc};
+        void* dev[] = {s.c.mbits, s.c.kbits, s.c.kocc, s.dblk, s.rblk, s.sbits, s.docc, s.dbits, s.rbits, s.zbits,
+                       s.fin, s.fsrc};
         for (void* p : dev)
             if (p) (void)hipFree(p);
         if (k == 0) {   // the contour filter's working arrays: one set, shared by the slots
@@ -498,8 +500,13 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
             s.c.gE = c0.gE;
             s.c.area2 = c0.area2;
         }
+        // rows of the kept mask with bits (k_paint -> dilate); KEEP_PLANES reads
+        // the kept mask back, so every row is written then
+        if ((e = dalloc(&s.c.kocc, H * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
+        s.c.kfull = (p.flags & DVC_FLAG_KEEP_PLANES) ? 1 : 0;
         if (h->fast) {   // block fields: u16 (B = 4) / u64 (B = 8) per block
             const size_t fb = p.block == 4 ? 2 : 8;
+            if ((e = dalloc(&s.docc, (size_t)h->NBY * mb)) != hipSuccess) return bad(e, "hipMalloc");
             if ((e = dalloc(&s.dblk, fb * nfield * mb)) != hipSuccess) return bad(e, "hipMalloc");
             if ((e = dalloc(&s.rblk, fb * nfield * mb)) != hipSuccess) return bad(e, "hipMalloc");
             if ((e = dalloc(&s.sbits, 8 * h->sstride * (size_t)mb)) != hipSuccess) return bad(e, "hipMalloc");
@@ -705,6 +712,9 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
 {
     Slot& S = h->slot[h->seq % NSLOT];
     hipStream_t s_ccl = h->stream;
+    // DVC_FD_SKIP (stage ablation for profiling only, results are wrong when
+    // set): bit 0 front, 1 contour filter, 2 dilate + accumulate, 3 output
+    static const int skip = [] { const char* e = getenv("DVC_FD_SKIP"); return e ? atoi(e) : 0; }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
     const uint8_t* d = nullptr;
     int dp = 0;
@@ -712,13 +722,14 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     dvc::SrcFmt sf{};
     int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs, crows, &sf);
     if (rc) return rc;
-    HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
-                             h->p.ithresh, h->s_front));
+    if (!(skip & 1))
+        HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
+                                 h->p.ithresh, h->s_front));
     HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
     HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_front, 0));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_acc, 0));
-    HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, s_ccl));
+    if (!(skip & 2)) HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, s_ccl));
     HIP_OK(hipEventRecord(S.ev_ccl, s_ccl));
     HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_ccl, 0));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_out, 0));
@@ -737,6 +748,8 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.obytes = (a.opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
     a.out_i420 = (h->p.flags & DVC_FLAG_OUT_I420) ? 1 : 0;
     a.kbits = S.c.kbits;
+    a.kocc = S.c.kocc;
+    a.docc = S.docc;
     a.dblk = S.dblk;
     a.rblk = S.rblk;
     a.sbits = S.sbits;
@@ -775,11 +788,11 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::launch_accumulate(a, h->s_acc));
+    if (!(skip & 4)) HIP_OK(dvc::launch_accumulate(a, h->s_acc));
     HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
     HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
-    HIP_OK(dvc::launch_out(a, h->s_out));
+    if (!(skip & 8)) HIP_OK(dvc::launch_out(a, h->s_out));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
         h->ev_used += 2;

@@ -44,13 +44,20 @@ struct CclBufs {
     uint32_t* area2;        // H x CAP 2*area per root
     uint64_t* kbits;        // H x WW kept (filtered) mask
     unsigned long long* stats;  // 64 slots x 4 counters (shared by all frames)
+    // Sparse masks (a surveillance frame is mostly still): nullable H bytes per
+    // frame, kocc[y] = kept row y has a bit set. With kocc, k_paint writes only
+    // the kept rows that have bits (kfull: every row, for plane read-back) and
+    // the dilate kernels read only those; without it every row is written.
+    uint8_t* kocc = nullptr;
+    int kfull = 0;
 
     __host__ __device__ static size_t bits_per_frame(const RowGeom& g) { return (size_t)g.H * g.WW; }
     __host__ __device__ CclBufs frame(size_t f, const RowGeom& g) const
     {
         const size_t nb = (size_t)g.H * g.WW, nr = (size_t)g.H * g.CAP, ng = (size_t)g.H * (g.CAP + 1);
         return CclBufs{mbits + f * nb, fbits + f * nb, rs + f * nr, re + f * nr, nfg + f * g.H, fpar + f * nr,
-                       gpar + f * (ng + 1), gE + f * ng, area2 + f * nr, kbits + f * nb, stats};
+                       gpar + f * (ng + 1), gE + f * ng, area2 + f * nr, kbits + f * nb, stats,
+                       kocc ? kocc + f * g.H : nullptr, kfull};
     }
     // bytes of every array for `frames` frames (host allocation)
     static void sizes(const RowGeom& g, size_t frames, size_t out[10])
@@ -96,6 +103,8 @@ struct BackArgs {
     int obytes;             // outputs not 4-byte aligned: byte stores
     int out_i420;           // outputs are I420 frames (W x H luma + two W/2 x H/2 chroma planes)
     const uint64_t* kbits;  // kept (filtered) masks from k_paint, H x WW per frame
+    const uint8_t* kocc;    // nullable: kept row has bits, H per frame (CclBufs::kocc); rows without are not read
+    uint8_t* docc;          // fast layout with kocc: block row by of frame t has dilated bits, docc[by * n + t]
     // fast layout
     void* dblk;             // dilated mask, block-major BxB bit fields per frame (k_dilate -> k_acc)
     void* rblk;             // acc > 127 per pixel, block-major BxB bit fields per frame (k_acc -> k_out)

@@ -583,8 +583,16 @@ __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t mi
         }
     }
     wave_sync_lds();
+    // rows without kept bits are only flagged (fb.kocc): most rows of a
+    // surveillance frame, whose zero words would cost a write here and a read
+    // in the dilation
+    unsigned long long any = 0;
     if (act)
+        for (int w = sl; w < g.WW; w += CG) any |= s_k[w];
+    for (int d = 1; d < CG; d <<= 1) any |= __shfl_xor(any, d, CG);
+    if (act && (any || !fb.kocc || fb.kfull))
         for (int w = sl; w < g.WW; w += CG) kbits[(size_t)y * g.WW + w] = s_k[w];
+    if (act && sl == 0 && fb.kocc) fb.kocc[y] = any ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- resolve ---
@@ -607,11 +615,13 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
     const int y = blockIdx.x * CG_ROWS + slot;
     const bool act = y < g.H;
     unsigned long long* s_f = lds_r + (size_t)slot * g.WW;
-    if (act)
+    // a row without runs is one gap touching both image borders: outside (E),
+    // its filled row is zero — k_area knows that from nfg and never reads it
+    const int n = act ? (int)nfg[y] : 0;
+    if (n)
         for (int w = sl; w < g.WW; w += CG) s_f[w] = mbits[(size_t)y * g.WW + w];
     wave_sync_lds();
     if (act) {
-        const int n = (int)nfg[y];
         const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
         for (int k = sl; k <= n; k += CG) {
             const int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
@@ -630,7 +640,7 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
         }
     }
     wave_sync_lds();
-    if (act)
+    if (n)
         for (int w = sl; w < g.WW; w += CG) fbits[(size_t)y * g.WW + w] = s_f[w];
 }
 
@@ -656,12 +666,14 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
     const bool act = y < g.H;
     unsigned long long* s_b = lds_b + (size_t)slot * g.WW;
     const bool last = y == g.H - 1;
-    if (act)
-        for (int w = sl; w < g.WW; w += CG) s_b[w] = last ? 0ull : fbits[(size_t)(y + 1) * g.WW + w];
+    const int n = act ? (int)nfg[y] : 0;
+    // F row y+1 (k_resolve): zero when row y+1 has no runs, not needed when row y has none
+    const bool fnext = n && !last && nfg[y + 1];
+    if (n)
+        for (int w = sl; w < g.WW; w += CG) s_b[w] = fnext ? fbits[(size_t)(y + 1) * g.WW + w] : 0ull;
     wave_sync_lds();
     int comps = 0;
     if (act) {
-        const int n = (int)nfg[y];
         const uint32_t base = (uint32_t)y * g.CAP;
         const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
         const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
@@ -740,6 +752,19 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
     const int wi = idx % WW, by = idx / WW, y0 = by * B;
     const int k = a.ksize, an = a.anchor;
     const uint64_t* kb = a.kbits + (size_t)t * H * WW;
+    // sparse masks (a.kocc): the rows of the window without kept bits are never
+    // read; a block row whose whole window is empty writes no fields, only
+    // docc = 0, and k_acc then reads none either
+    const uint8_t* ko = a.kocc ? a.kocc + (size_t)t * H : nullptr;
+    if (ko) {
+        int any = 0;
+        for (int r = 0; r < B + k - 1; ++r) {
+            const int y = y0 - an + r;
+            if (y >= 0 && y < H) any |= ko[y];
+        }
+        if (wi == 0) a.docc[(size_t)by * a.n + t] = (uint8_t)any;
+        if (!any && !(a.dbg_dil && t == a.n - 1)) return;
+    }
     // pixels past W (the last word) are not pixels: their dilated bits stay 0
     const uint64_t vmask = (wi == WW - 1 && (W & 63)) ? (1ull << (W & 63)) - 1ull : ~0ull;
     uint64_t out[B];
@@ -747,7 +772,7 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
     for (int i = 0; i < B; ++i) out[i] = 0;
     for (int r = 0; r < B + k - 1; ++r) {
         const int y = y0 - an + r;
-        if (y < 0 || y >= H) continue;
+        if (y < 0 || y >= H || (ko && !ko[y])) continue;
         const uint64_t* row = kb + (size_t)y * WW;
         const uint64_t c = row[wi], pv = wi > 0 ? row[wi - 1] : 0ull, nv = wi + 1 < WW ? row[wi + 1] : 0ull;
         uint64_t o = c;
@@ -804,9 +829,15 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     BT* rb = reinterpret_cast<BT*>(a.rblk);
     constexpr int U = 8;
     BT dA[U], dB[U];
+    // docc (uniform over the workgroup's block row): frames whose block row has
+    // no dilated bit load no field
+    const uint8_t* dc = a.docc ? a.docc + (size_t)by * a.n : nullptr;
     auto load_chunk = [&](int t0, BT (&dst)[U]) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[u] = db[(size_t)min(t0 + u, a.n - 1) * NB + blk];   // clamped: unconditional
+        for (int u = 0; u < U; ++u) {
+            const int tt = min(t0 + u, a.n - 1);   // clamped: the last frames reload
+            dst[u] = (!dc || dc[tt]) ? db[(size_t)tt * NB + blk] : (BT)0;
+        }
     };
     unsigned long long nstatic = 0;
     const float dil0 = __builtin_fmaf(0.f, a.beta, a.gamma), dil1 = __builtin_fmaf(255.f, a.beta, a.gamma);
@@ -852,7 +883,9 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
                 const uint32_t m = ((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u);
                 r |= (BT)((BT)m << (B * i + 4 * q));
             }
-        if (active) rb[(size_t)t * NB + blk] = r;
+        // a static block (acc all zero) has no acc > 127 bit: its field is not
+        // written, k_out / k_out_gen take it as zero from sbits
+        if (active && !zero) rb[(size_t)t * NB + blk] = r;
         const unsigned long long sb = __ballot(active && zero);
         if (lane == 0) a.sbits[(size_t)t * a.sstride + (size_t)by * a.SW + blockIdx.x] = sb;
         nstatic += (unsigned long long)__popcll(sb);
@@ -989,7 +1022,8 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
     if (a.overlay) {
         typedef typename BlkT<B>::T BT;
         const int NBX = a.NBX;
-        const BT rf = reinterpret_cast<const BT*>(a.rblk)[(size_t)t * a.NBY * NBX + (size_t)(by / B) * NBX + bx / B];
+        const BT rf = is_static ? (BT)0
+                                : reinterpret_cast<const BT*>(a.rblk)[(size_t)t * a.NBY * NBX + (size_t)(by / B) * NBX + bx / B];
         uint32_t red[B];
         const bool rany = rf != 0;
 #pragma unroll
@@ -1154,7 +1188,7 @@ __global__ void __launch_bounds__(256) k_dilate_rows(BackArgs a)
     uint64_t out = 0;
     for (int r = 0; r < k; ++r) {
         const int yy = y - an + r;
-        if (yy < 0 || yy >= H) continue;
+        if (yy < 0 || yy >= H || (a.kocc && !a.kocc[(size_t)t * H + yy])) continue;
         const uint64_t* row = kb + (size_t)yy * WW;
         const uint64_t c = row[wi], pv = wi > 0 ? row[wi - 1] : 0ull, nv = wi + 1 < WW ? row[wi + 1] : 0ull;
         uint64_t o = c;
@@ -1289,11 +1323,12 @@ __global__ void __launch_bounds__(256) k_out_gen(BackArgs a, GenRegion R, int fa
         }
         if (a.overlay) {
             bool red;
-            if (fast) {
+            if (fast) {   // static blocks' fields are not written (k_acc): zero
                 const size_t fi = (size_t)t * a.NBY * a.NBX + (size_t)(y / B) * a.NBX + x / B;
                 const int bit = (y % B) * B + x % B;
-                red = B == 4 ? (reinterpret_cast<const uint16_t*>(a.rblk)[fi] >> bit) & 1
-                             : (reinterpret_cast<const uint64_t*>(a.rblk)[fi] >> bit) & 1ull;
+                red = flag[b] == 0 &&
+                      (B == 4 ? (reinterpret_cast<const uint16_t*>(a.rblk)[fi] >> bit) & 1
+                              : (reinterpret_cast<const uint64_t*>(a.rblk)[fi] >> bit) & 1ull);
             } else {
                 red = (a.rbits[(size_t)t * plane + (size_t)y * WW + (x >> 6)] >> (x & 63)) & 1ull;
             }
