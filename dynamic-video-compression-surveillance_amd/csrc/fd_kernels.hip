@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
 // against the global ids, so "root = smallest id" carries over. When the band
 // has more nodes than the LDS budget (`budget`, e.g. pure-noise masks), the same
 // unions run on the global parent arrays instead (monotone atomicMin links).
-// Small workgroups (4 waves, <= 32 KB LDS) keep the band stage schedulable
+// Small workgroups (4 waves, ~14 KB LDS at 1080p) keep the band stage schedulable
 // beside the streaming kernels of the other two streams. Dynamic LDS: band_lds().
 constexpr int BG = 16, BAND_ROWS = 256 / BG;
 
@@ -1517,10 +1517,16 @@ size_t band_lds(const RowGeom& g, int bh, int budget)
 
 int band_rows(const RowGeom&) { return BAND_ROWS; }
 
-// Node budget of a band: what fits in 32 KB of LDS, at least 1024.
+// Node budget of a band: 1024 (4 KB of parents beside the run index, ~14 KB
+// per workgroup at 1080p) — bands with more runs and gaps (noise) take the
+// global-array path. Interleaved A/B at 1080p against round 1's 32 KB of LDS
+// per workgroup: clean 310.0 k vs 310.5 k Mpx/s, noisy 277.0 k vs 270.3 k
+// (more band workgroups resident beside k_front's LDS tiles).
+// DVC_BAND_LDS_KB sizes it by total LDS instead (sweeps).
 static int band_budget(const RowGeom& g)
 {
-    const long long rest = 32 * 1024 - (long long)band_lds(g, BAND_ROWS, 0);
+    static const int kb = [] { const char* e = getenv("DVC_BAND_LDS_KB"); return e ? std::max(8, atoi(e)) : 0; }();
+    const long long rest = kb * 1024LL - (long long)band_lds(g, BAND_ROWS, 0);
     return (int)std::max<long long>(1024, rest / 4);
 }
 

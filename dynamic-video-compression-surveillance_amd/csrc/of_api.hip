@@ -507,6 +507,10 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // overwrites R slots that only flow(i-2) reads; with RB = window + 2 mb the
     // raw bits flow(i) writes are the evictions only vote(i-2) reads
     OfSlot& S = h->slot[h->seq & 1];
+    // DVC_OF_SKIP (stage ablation for profiling only, results are wrong when
+    // set): bit 1 flow, 2 vote + mask morphology / rectangles, 3 k_of_out (the
+    // pyramid always runs: the flow kernels index R by the flow)
+    static const int skip = [] { const char* e = getenv("DVC_OF_SKIP"); return e ? atoi(e) : 0; }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
     if (h->fmt != DVC_FMT_BGR) {
         // 4:2:0 surfaces -> BGR in the slot's frames (of:66,145), read by the
@@ -530,16 +534,16 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
             h->ev.push_back(e);
         }
     }
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow, &h->epoch));
+    if (!(skip & 2)) HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow, &h->epoch));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_flow));
-    HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch));
+    if (!(skip & 2)) HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_flow));
         h->ev_used += 2;
     }
     HIP_OK(hipEventRecord(S.ev_flow, h->s_flow));
     HIP_OK(hipStreamWaitEvent(h->s_mask, S.ev_flow, 0));
-    HIP_OK(dvc::of_launch_mask(h->g, h->b, a0, h->p.window, n, h->s_mask));
+    if (!(skip & 4)) HIP_OK(dvc::of_launch_mask(h->g, h->b, a0, h->p.window, n, h->s_mask));
     dvc::OfOutArgs o{};
     o.bgr = d;
     o.pitch = dp;
@@ -551,7 +555,7 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     o.quant = h->p.quant;
     o.qinv = 1.0 / (double)h->p.quant;
     o.M = h->M;
-    HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->s_mask));
+    if (!(skip & 8)) HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->s_mask));
     HIP_OK(hipEventRecord(S.ev_mask, h->s_mask));
     S.recorded = true;
     h->seq++;
