@@ -27,7 +27,8 @@ import os
 import time
 
 from . import video_io
-from ._native import DVC_E_ODD_DCT, DvcError, pinned
+from ._dropin import ChunkPipeline
+from ._native import DVC_E_ODD_DCT, DvcError
 from .fd import FDWorker
 
 LOG_FORMAT = "%(asctime)s - %(levelname)s - %(message)s"
@@ -55,19 +56,23 @@ def _feed_dir(output_dir, video_path) -> str:
 
 
 class _Writers:
-    """The two mp4v outputs of fd:63-65 plus the progress callback of fd:137-138."""
+    """The two mp4v outputs of fd:63-65 plus the progress callback of fd:137-138.
+    ``yuv``: both sinks are Y4M videos and take the worker's I420 frames as they
+    are (no BGR round trip through the host)."""
 
     def __init__(self, out_dir, fps, size, progress_callback):
         self.mask = video_io.open_sink(os.path.join(out_dir, "dilated_motion_mask_video.mp4"), fps, size)
         self.final = video_io.open_sink(os.path.join(out_dir, "compressed_final_video.mp4"), fps, size)
         self.callback = progress_callback
         self.frames = 0
+        self.yuv = isinstance(self.mask, video_io.Y4mWriter) and isinstance(self.final, video_io.Y4mWriter)
 
     def emit(self, overlay, compressed):
-        self.mask.write(overlay)
+        put = (lambda s, f: s.write_yuv(f)) if self.yuv else (lambda s, f: s.write(f))
+        put(self.mask, overlay)
         if compressed is None:       # the frame whose block loop raised: overlay only (fd:112 < fd:122)
             return
-        self.final.write(compressed)
+        put(self.final, compressed)
         self.frames += 1
         if self.callback is not None and self.frames % 50 == 0:
             self.callback(self.frames)
@@ -116,46 +121,60 @@ def filter_and_dilate_movements(video_path, output_dir,
 
     per_frame_s = []
     worker = None
+    reader = writer = None
     try:
         R = max(1, READ_AHEAD)
+        blk = block_size
+        i420 = sinks.yuv and blk in (4, 8) and out_w % blk == 0 and out_h % blk == 0
         worker = FDWorker(out_w, out_h, device=_device(), src_width=src_w, src_height=src_h, max_batch=R,
                           block_size=block_size, motion_threshold=motion_threshold, min_area=min_area,
                           kernel_size=kernel_size, release_factor=release_factor,
-                          quantization_level=quantization_level, in_format=cap.pixel_format if yuv else "BGR")
+                          quantization_level=quantization_level, in_format=cap.pixel_format if yuv else "BGR",
+                          out_format="I420" if i420 else "BGR")
+        if not i420:
+            sinks.yuv = False
         worker.prime(first)                                     # fd:67-81 (resize on the GPU)
-        frames = pinned((R,) + worker._fshape)
-        overlay, compressed = pinned((R, out_h, out_w, 3)), pinned((R, out_h, out_w, 3))
-        eof = False
-        while not eof:
-            t0 = time.time()
-            n = 0
-            while n < R:                                        # fd:87-89
-                ok, f = read()
-                if not ok:
-                    eof = True
-                    break
-                frames[n] = f
-                n += 1
+
+        def emit(i, ov_cp, done, failing):                      # writer thread: fd:112,131,137-138
+            ov, cp = ov_cp
+            for t in range(done):
+                sinks.emit(ov[t], cp[t])
+            if failing:
+                sinks.emit(ov[done], None)
+
+        pipe = ChunkPipeline(R, worker._fshape, [worker._oshape, worker._oshape], read, emit)
+        reader, writer = pipe.start()
+        handed = 0                                              # frames given to the writer
+        while True:
+            i, n = pipe.next_chunk()                            # fd:87-89, R frames ahead
             if n == 0:
                 break
+            j = pipe.out_buffer()
+            ov, cp = pipe.outs[j]
+            t0 = time.time()
             stop = None
             try:                                                # fd:91-133, n times
-                worker.step_batch(frames[:n], overlay[:n], compressed[:n])
+                worker.step_batch(pipe.ins[i][:n], ov[:n], cp[:n])
                 done = n
             except DvcError as e:
                 if e.code != DVC_E_ODD_DCT:
                     raise
-                stop, done = e, worker.stats()["frames"] - sinks.frames
-            for t in range(done):
-                sinks.emit(overlay[t], compressed[t])
+                stop, done = e, worker.stats()["frames"] - handed
             per_frame_s.extend([(time.time() - t0) / n] * done)
+            pipe.write(i, j, done, stop is not None)
+            handed += done
             if stop is not None:
-                sinks.emit(overlay[done], None)
+                pipe.finish()
                 raise RuntimeError("OpenCV(4.11.0) (-213:The function/feature is not implemented) "
                                    "Odd-size DCT's are not implemented in function 'apply'") from stop
+            if n < R:
+                break
+        pipe.finish()
     except Exception as e:
         logging.error("Error during processing: " + str(e), exc_info=True)
     finally:
+        if reader is not None:
+            pipe.stop()
         cap.release()
         sinks.release()
         if worker is not None:

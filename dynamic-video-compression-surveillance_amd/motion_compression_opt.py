@@ -30,6 +30,7 @@ import time
 import numpy as np
 
 from . import _native as N
+from ._dropin import ChunkPipeline
 from . import video_io
 from .of import OFWorker
 
@@ -88,38 +89,41 @@ def temporal_smoothing_flow(video_path, output_dir, flow_threshold=0.5, alpha_fr
         cap.release()
         return 0, 0, 0
     frame_count = 0
-    worker = None
+    worker = pipe = None
     try:
         # of:65-101 for READ_AHEAD frames per dvc_of_step_batch call (identical
-        # to one step per frame): the frames are read ahead into page-locked
-        # buffers and the masks come back in one copy per group
+        # to one step per frame): a reader thread reads ahead into page-locked
+        # chunks, a writer thread writes the overlay (the frames themselves,
+        # of:99) and mask videos while the next chunk runs (_dropin.py)
         R = max(1, READ_AHEAD)
         worker = OFWorker(width, height, device=_device(), flow_threshold=flow_threshold,
                           alpha_fraction=alpha_fraction, window_size=window_size, morph_kernel=morph_kernel,
                           max_batch=R)
         worker.prime(first_frame)
-        frames = N.pinned((R, height, width, 3))
-        masks = N.pinned((R, height, width))
-        eof = False
-        while not eof:
-            n = 0
-            while n < R:
-                ret, frame = cap.read()
-                if not ret:
-                    eof = True
-                    break
-                frames[n] = frame
-                n += 1
+
+        def emit(i, outs, done, failing):
+            for t in range(done):
+                out_overlay.write(pipe.ins[i][t])
+                out_mask.write(outs[0][t])
+
+        pipe = ChunkPipeline(R, (height, width, 3), [(height, width)], cap.read, emit)
+        pipe.start()
+        while True:
+            i, n = pipe.next_chunk()
             if n == 0:
                 break
-            worker.step_batch(frames[:n], mask=masks[:n], want=("mask",))
-            for t in range(n):
-                out_overlay.write(frames[t])
-                out_mask.write(masks[t])
+            j = pipe.out_buffer()
+            worker.step_batch(pipe.ins[i][:n], mask=pipe.outs[j][0][:n], want=("mask",))
+            pipe.write(i, j, n)
             frame_count += n
+            if n < R:
+                break
+        pipe.finish()
     except Exception as e:
         logging.error(f"Error during motion detection: {e}", exc_info=True)
     finally:
+        if pipe is not None:
+            pipe.stop()
         cap.release()
         out_overlay.release()
         out_mask.release()

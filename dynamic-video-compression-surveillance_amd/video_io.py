@@ -193,6 +193,18 @@ class Y4mWriter:
         self._fp.write(payload.tobytes())
         self.n += 1
 
+    def write_yuv(self, frame: np.ndarray) -> None:
+        """A frame already in the stream's layout: (H*3/2, W) I420 for colour
+        streams (e.g. the FD worker's DVC_FLAG_OUT_I420 outputs), (H, W) mono."""
+        if self._fp is None:
+            return
+        exp = (self.H * 3 // 2, self.W) if self.is_color else (self.H, self.W)
+        if frame.shape != exp:
+            return
+        self._fp.write(b"FRAME\n")
+        self._fp.write(np.ascontiguousarray(frame, dtype=np.uint8).tobytes())
+        self.n += 1
+
     def release(self) -> None:
         if self._fp is not None:
             self._fp.close()

@@ -268,6 +268,46 @@ def test_process_single_video_fd(gpu_lib, tmp_path):
     assert (d / "processing.log").exists()
 
 
+def test_process_single_video_fd_chunks_and_odd_dct_stop(gpu_lib, tmp_path, monkeypatch, caplog):
+    """The drop-in's reader / step / writer threads: chunks of 4 frames give the
+    same output videos as one FDWorker.step per frame; a 3-px edge block stops
+    the run as the reference does (fd:122, fd:140): the failing frame's overlay
+    is written, its compressed frame is not, the error is logged."""
+    from dvc_amd import frame_differencing as fdm
+    from dvc_amd._native import DVC_E_ODD_DCT, DvcError
+    from dvc_amd.synthetic import clip
+    monkeypatch.setattr(fdm, "READ_AHEAD", 4)
+
+    def per_frame(frames):
+        w = gpu_lib.FDWorker(frames.shape[2], frames.shape[1])
+        w.prime(frames[0])
+        outs = []
+        try:
+            for f in frames[1:]:
+                outs.append(w.step(f))
+        except DvcError as e:
+            assert e.code == DVC_E_ODD_DCT
+            return outs, True
+        finally:
+            w.close()
+        return outs, False
+
+    for name, frames in (("cam", clip(320, 240, 11, seed=5)), ("odd", clip(643, 360, 12, seed=1003, n_objects=4))):
+        np.save(tmp_path / f"{name}.npy", frames)
+        fdm.process_single_video_fd(str(tmp_path / f"{name}.npy"), str(tmp_path / "out"))
+        ref, stopped = per_frame(frames)
+        ov = np.load(tmp_path / f"out/{name}/dilated_motion_mask_video.npy")
+        cp = np.load(tmp_path / f"out/{name}/compressed_final_video.npy")
+        assert len(cp) == len(ref) and len(ov) == len(ref) + (1 if stopped else 0)
+        for t in range(len(ref)):
+            assert np.array_equal(ov[t], ref[t][0]) and np.array_equal(cp[t], ref[t][1]), f"{name} frame {t + 1}"
+        assert stopped == (name == "odd")
+        if stopped:   # logged, not raised (fd:140-141); processing.log only if logging was unconfigured
+            assert "Odd-size DCT" in caplog.text
+        txt = (tmp_path / f"out/{name}/execution_times.txt").read_text()
+        assert f"Frames processed: {len(cp)}" in txt
+
+
 # ---------------------------------------------------------------- geometry ---
 # Any frame size and block size (fd:117-127: partial edge blocks are their
 # slices; an odd side > 1 of a static block stops the reference, fd:122/140),
