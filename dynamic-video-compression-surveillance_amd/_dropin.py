@@ -21,13 +21,15 @@ from ._native import pinned
 class ChunkPipeline:
     NBUF = 3
 
-    def __init__(self, R, in_shape, out_shapes, read, emit):
+    def __init__(self, R, in_shape, out_shapes, read, emit, alloc=None):
         """``read()`` -> (ok, frame) (cap.read); ``emit(i, outs, done, failing)``
         writes the first ``done`` frames of input chunk ``i`` / output buffers
-        ``outs`` (on the writer thread)."""
+        ``outs`` (on the writer thread). ``alloc(shape)``: the buffers, default
+        page-locked uint8 arrays (``_native.pinned``)."""
         self.R, self.read, self.emit = R, read, emit
-        self.ins = [pinned((R,) + tuple(in_shape)) for _ in range(self.NBUF)]
-        self.outs = [tuple(pinned((R,) + tuple(s)) for s in out_shapes) for _ in range(self.NBUF)]
+        alloc = alloc or pinned
+        self.ins = [alloc((R,) + tuple(in_shape)) for _ in range(self.NBUF)]
+        self.outs = [tuple(alloc((R,) + tuple(s)) for s in out_shapes) for _ in range(self.NBUF)]
         self.free_in, self.free_out = queue.Queue(), queue.Queue()
         for k in range(self.NBUF):
             self.free_in.put(k)
@@ -74,10 +76,11 @@ class ChunkPipeline:
                 self.emit(i, self.outs[j], done, failing)
                 self.free_out.put(j)
                 self.free_in.put(i)
-        except Exception as e:           # surfaced by out_buffer / finish
+        except Exception as e:           # surfaced by next_chunk / out_buffer / finish
             self.error = e
             self.free_out.put(None)
-            self.free_in.put(None)
+            self.free_in.put(None)       # the reader stops
+            self.filled.put((None, 0))   # a caller waiting for a chunk wakes up
 
     def next_chunk(self):
         """(input chunk index, frames in it); 0 frames at the end of the video."""
