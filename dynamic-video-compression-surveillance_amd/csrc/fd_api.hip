@@ -714,7 +714,12 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     hipStream_t s_ccl = h->stream;
     // DVC_FD_SKIP (stage ablation for profiling only, results are wrong when
     // set): bit 0 front, 1 contour filter, 2 dilate + accumulate, 3 output
-    static const int skip = [] { const char* e = getenv("DVC_FD_SKIP"); return e ? atoi(e) : 0; }();
+    static const int skip = [] {
+        const char* e = getenv("DVC_FD_SKIP");
+        const int v = e ? atoi(e) : 0;
+        if (v) std::fprintf(stderr, "dvc: DVC_FD_SKIP=%d set: stages skipped, outputs are wrong (profiling only)\n", v);
+        return v;
+    }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
     const uint8_t* d = nullptr;
     int dp = 0;

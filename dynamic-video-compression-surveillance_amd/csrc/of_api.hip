@@ -8,6 +8,7 @@
 // here with the same expressions as oracle/of_oracle.c.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <cstdio>
 
 #include <cfloat>
 #include <cmath>
@@ -510,7 +511,12 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // DVC_OF_SKIP (stage ablation for profiling only, results are wrong when
     // set): bit 1 flow, 2 vote + mask morphology / rectangles, 3 k_of_out (the
     // pyramid always runs: the flow kernels index R by the flow)
-    static const int skip = [] { const char* e = getenv("DVC_OF_SKIP"); return e ? atoi(e) : 0; }();
+    static const int skip = [] {
+        const char* e = getenv("DVC_OF_SKIP");
+        const int v = e ? atoi(e) : 0;
+        if (v) std::fprintf(stderr, "dvc: DVC_OF_SKIP=%d set: stages skipped, outputs are wrong (profiling only)\n", v);
+        return v;
+    }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
     if (h->fmt != DVC_FMT_BGR) {
         // 4:2:0 surfaces -> BGR in the slot's frames (of:66,145), read by the
