@@ -410,6 +410,14 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
     }
     __syncthreads();
     const int RT = s_roff[BH];
+    if (RT == 0) {   // uniform: a band without runs — each row is one border gap, outside
+        if (act && sl == 0) {
+            gpar[gbase] = 0u;
+            nfg[y] = 0u;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;
+        return;
+    }
     const bool local = 1 + RT + s_goff[BH] <= budget;   // uniform
     const bool left_bg = act && !(st[0] & 1ull);
     const bool right_bg = act && !((en[(W - 1) >> 6] >> ((W - 1) & 63)) & 1ull);
@@ -621,7 +629,9 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
     if (n)
         for (int w = sl; w < g.WW; w += CG) s_f[w] = mbits[(size_t)y * g.WW + w];
     wave_sync_lds();
-    if (act) {
+    // (no runs: the row's one gap is the border gap k_band already tied to
+    // OUTSIDE, and no kernel reads its gE)
+    if (n) {
         const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
         for (int k = sl; k <= n; k += CG) {
             const int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
