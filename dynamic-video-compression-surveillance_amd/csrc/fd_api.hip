@@ -200,7 +200,7 @@ static void free_all(dvc_fd* h)
         for (void* p : dev)
             if (p) (void)hipFree(p);
         if (k == 0) {   // the contour filter's working arrays: one set, shared by the slots
-            void* shared[] = {s.c.fbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE};
+            void* shared[] = {s.c.fbits, s.c.rs, s.c.re, s.c.nfg, s.c.fpar, s.c.gpar, s.c.area2, s.c.gE, s.c.rowb};
             for (void* p : shared)
                 if (p) (void)hipFree(p);
         }
@@ -489,8 +489,11 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
             if (shared && k > 0) continue;   // slot 0's, set below
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
         }
+        if (k == 0 && (e = dalloc(&s.c.rowb, dvc::CclBufs::rowb_bytes(h->g, mb))) != hipSuccess)
+            return bad(e, "hipMalloc");
         if (k > 0) {
             const dvc::CclBufs& c0 = h->slot[0].c;
+            s.c.rowb = c0.rowb;
             s.c.fbits = c0.fbits;
             s.c.rs = c0.rs;
             s.c.re = c0.re;
@@ -1047,6 +1050,7 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
     uint32_t* gpar = (uint32_t*)alloc(4 * (1 + H * (CAP + 1)));
     uint8_t* gE = (uint8_t*)alloc(H * (CAP + 1));
     uint32_t* area2 = (uint32_t*)alloc(4 * H * CAP);
+    uint32_t* rowb = (uint32_t*)alloc(8 * H);
     unsigned long long* stats = (unsigned long long*)alloc(8 * 4 * 64);
     int rc = DVC_OK;
     auto done = [&]() { for (void* p : owned) (void)hipFree(p); };
@@ -1058,6 +1062,7 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
     if (e == hipSuccess) e = hipMemset(gpar, 0, 4 * (1 + H * (CAP + 1)));
     if (e == hipSuccess) {
         dvc::CclBufs c{mbits, fbits, rs, re, nfg, fpar, gpar, gE, area2, kept, stats};
+        c.rowb = rowb;
         e = dvc::launch_ccl(c, g, 1, min_area2, s);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();

@@ -50,6 +50,12 @@ struct CclBufs {
     // the dilate kernels read only those; without it every row is written.
     uint8_t* kocc = nullptr;
     int kfull = 0;
+    // Run index packed per band (k_band): the runs of band b's rows are nodes
+    // b*16*CAP + (runs of the band's earlier rows) + k, its gaps 1 + b*16*(CAP+1)
+    // + (gaps of earlier rows) + k; rowb[2y], rowb[2y+1] = the first run / gap
+    // node of row y (2 x H per frame). A band's few runs share cache lines.
+    uint32_t* rowb = nullptr;
+    static size_t rowb_bytes(const RowGeom& g, size_t frames) { return (size_t)8 * g.H * frames; }
 
     __host__ __device__ static size_t bits_per_frame(const RowGeom& g) { return (size_t)g.H * g.WW; }
     __host__ __device__ CclBufs frame(size_t f, const RowGeom& g) const
@@ -57,7 +63,7 @@ struct CclBufs {
         const size_t nb = (size_t)g.H * g.WW, nr = (size_t)g.H * g.CAP, ng = (size_t)g.H * (g.CAP + 1);
         return CclBufs{mbits + f * nb, fbits + f * nb, rs + f * nr, re + f * nr, nfg + f * g.H, fpar + f * nr,
                        gpar + f * (ng + 1), gE + f * ng, area2 + f * nr, kbits + f * nb, stats,
-                       kocc ? kocc + f * g.H : nullptr, kfull};
+                       kocc ? kocc + f * g.H : nullptr, kfull, rowb + f * 2 * g.H};
     }
     // bytes of every array for `frames` frames (host allocation)
     static void sizes(const RowGeom& g, size_t frames, size_t out[10])

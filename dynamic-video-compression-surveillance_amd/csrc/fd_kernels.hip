@@ -374,25 +374,17 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
     const int y0 = blockIdx.x * BH, y = y0 + slot;
     const bool act = y < g.H;
     const uint32_t CAP = (uint32_t)g.CAP;
-    const uint32_t base = (uint32_t)y * CAP, gbase = 1u + (uint32_t)y * (CAP + 1);
+    // the band's node ranges (CclBufs::rowb): runs RB0.., gaps GB0..
+    const uint32_t RB0 = (uint32_t)blockIdx.x * BH * CAP, GB0 = 1u + (uint32_t)blockIdx.x * BH * (CAP + 1);
     uint64_t* st = l_st + slot * WW;
     uint64_t* en = l_en + slot * WW;
     uint16_t* ps = l_ps + slot * (WW + 1);
     uint16_t* pe = l_pe + slot * (WW + 1);
 
-    // ---- phase 1: run index of row y in LDS; runs to global (later kernels)
+    // ---- phase 1: run index of row y in LDS
     int n = 0;
     unsigned long long motion = 0;
-    if (act) {
-        const uint64_t* row = mbits + (size_t)y * WW;
-        n = build_row_idx_g<BG>(row, WW, W, st, en, ps, pe, &motion);
-        for (int i = sl; i < WW; i += BG) {
-            uint64_t s = st[i], e = en[i];
-            int ks = ps[i], ke = pe[i];
-            while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
-            while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
-        }
-    }
+    if (act) n = build_row_idx_g<BG>(mbits + (size_t)y * WW, WW, W, st, en, ps, pe, &motion);
     if (sl == 0) s_n[slot] = act ? n : 0;
     for (int d = 32; d >= 1; d >>= 1) motion += __shfl_xor(motion, d, 64);   // the wave's 4 rows
     if ((threadIdx.x & 63) == 0 && motion) atomicAdd(stats + STAT_SLOT(y) * 4 + 1, motion);
@@ -410,6 +402,11 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
     }
     __syncthreads();
     const int RT = s_roff[BH];
+    const uint32_t base = RB0 + (uint32_t)s_roff[slot], gbase = GB0 + (uint32_t)s_goff[slot];
+    if (act && sl == 0) {
+        fb.rowb[2 * y] = base;
+        fb.rowb[2 * y + 1] = gbase;
+    }
     if (RT == 0) {   // uniform: a band without runs — each row is one border gap, outside
         if (act && sl == 0) {
             gpar[gbase] = 0u;
@@ -418,6 +415,14 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
         if (blockIdx.x == 0 && threadIdx.x == 0) gpar[0] = 0;
         return;
     }
+    // the row's runs to global (later kernels), packed after the band's earlier rows
+    if (act)
+        for (int i = sl; i < WW; i += BG) {
+            uint64_t s = st[i], e = en[i];
+            int ks = ps[i], ke = pe[i];
+            while (s) { rs[base + ks++] = (uint16_t)(i * 64 + __builtin_ctzll(s)); s &= s - 1; }
+            while (e) { re[base + ke++] = (uint16_t)(i * 64 + __builtin_ctzll(e)); e &= e - 1; }
+        }
     const bool local = 1 + RT + s_goff[BH] <= budget;   // uniform
     const bool left_bg = act && !(st[0] & 1ull);
     const bool right_bg = act && !((en[(W - 1) >> 6] >> ((W - 1) & 63)) & 1ull);
@@ -443,28 +448,16 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
                                 [&](int i, int j) { lunion(lp, GP + i, q1 + j); });
         }
         __syncthreads();
-        // ---- phase 3: flatten; publish band-local roots as global ids
-        auto row_of = [&](const int* off, uint32_t v) {   // largest r with off[r] <= v
-            int r = 0;
-            for (int q = 1; q < BH; ++q) r = (uint32_t)off[q] <= v ? q : r;
-            return r;
-        };
+        // ---- phase 3: flatten; publish band-local roots as global ids (the
+        // local numbering is the band's packed global numbering minus RB0 / GB0)
         if (act) {
             for (int k = sl; k < n; k += BG) {
-                const uint32_t l = lfind(lp, FG + k) - 1;
-                const int rr = row_of(s_roff, l);
-                fpar[base + k] = (uint32_t)(y0 + rr) * CAP + (l - s_roff[rr]);
+                fpar[base + k] = RB0 + (lfind(lp, FG + k) - 1);
                 area2[base + k] = 0;
             }
             for (int k = sl; k <= n; k += BG) {
                 const uint32_t r = lfind(lp, GP + k);
-                uint32_t gid = 0;
-                if (r != 0) {
-                    const uint32_t l = r - 1 - RT;
-                    const int rr = row_of(s_goff, l);
-                    gid = 1u + (uint32_t)(y0 + rr) * (CAP + 1) + (l - s_goff[rr]);
-                }
-                gpar[gbase + k] = gid;
+                gpar[gbase + k] = r != 0 ? GB0 + (r - 1 - RT) : 0u;
             }
         }
     } else {
@@ -480,7 +473,7 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
         __threadfence_block();
         __syncthreads();
         if (act && slot + 1 < BH && y + 1 < g.H) {
-            const uint32_t b1 = base + CAP, g1 = gbase + CAP + 1;
+            const uint32_t b1 = RB0 + (uint32_t)s_roff[slot + 1], g1 = GB0 + (uint32_t)s_goff[slot + 1];
             const RowIdx r0{st, en, ps, pe}, r1{st + WW, en + WW, ps + WW + 1, pe + WW + 1};
             row_pair_unions<BG>(W, WW, r0, n, r1,
                                 [&](int i, int j) { uf_union(fpar, base + i, b1 + j); },
@@ -524,8 +517,7 @@ __global__ void __launch_bounds__(256) k_merge(CclBufs cb, RowGeom g, int BH)
     }
     wave_sync_lds();
     if (!act) return;
-    const uint32_t b0 = (uint32_t)y * g.CAP, b1 = b0 + g.CAP;
-    const uint32_t g0 = 1u + (uint32_t)y * (g.CAP + 1), g1 = g0 + (g.CAP + 1);
+    const uint32_t b0 = fb.rowb[2 * y], b1 = fb.rowb[2 * y + 2], g0 = fb.rowb[2 * y + 1], g1 = fb.rowb[2 * y + 3];
     for (int i = sl; i < n0; i += MG) {
         const int a = select_k(st, ps, WW, i), b = select_k(en, pe, WW, i);
         const int j0 = rank_le(en + WW, pe + WW + 1, WW, a - 2), j1 = rank_le(st + WW, ps + WW + 1, WW, b + 1);
@@ -580,8 +572,8 @@ __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t mi
     wave_sync_lds();
     if (act) {
         const int n = (int)nfg[y];
-        const uint32_t base = (uint32_t)y * g.CAP;
-        const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
+        const uint32_t base = fb.rowb[2 * y];
+        const uint8_t* ge = gE + (fb.rowb[2 * y + 1] - 1);   // gap node g at gE[g - 1]
         for (int k = sl; k < n; k += CG) {
             const uint32_t root = fpar[base + k];
             if (!((int64_t)area2[root] > min_area2)) continue;  // contourArea > min_area
@@ -632,7 +624,7 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
     // (no runs: the row's one gap is the border gap k_band already tied to
     // OUTSIDE, and no kernel reads its gE)
     if (n) {
-        const uint32_t base = (uint32_t)y * g.CAP, gbase = 1u + (uint32_t)y * (g.CAP + 1);
+        const uint32_t base = fb.rowb[2 * y], gbase = fb.rowb[2 * y + 1];
         for (int k = sl; k <= n; k += CG) {
             const int a = k == 0 ? 0 : (int)re[base + k - 1] + 1;
             const int b = k == n ? g.W - 1 : (int)rs[base + k] - 1;
@@ -646,7 +638,7 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
                     paint_bits(s_f, 0, g.WW, a, b);
                 }
             }
-            gE[(size_t)y * (g.CAP + 1) + k] = e;
+            gE[gbase - 1 + k] = e;
         }
     }
     wave_sync_lds();
@@ -684,8 +676,8 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
     wave_sync_lds();
     int comps = 0;
     if (act) {
-        const uint32_t base = (uint32_t)y * g.CAP;
-        const uint8_t* ge = gE + (size_t)y * (g.CAP + 1);
+        const uint32_t base = fb.rowb[2 * y];
+        const uint8_t* ge = gE + (fb.rowb[2 * y + 1] - 1);
         const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
         const unsigned long long gmask = 0xffffull << g0;
         for (int k0 = 0; k0 < n; k0 += CG) {   // uniform trip count within the group: it reduces below

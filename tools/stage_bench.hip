@@ -59,6 +59,7 @@ int main(int argc, char** argv)
                        (void**)&c.fpar, (void**)&c.gpar, (void**)&c.gE, (void**)&c.area2, (void**)&c.kbits};
     for (int i = 0; i < 10; ++i) CK(hipMalloc(ptrs[i], sz[i]));
     CK(hipMemset(c.gpar, 0, sz[6]));
+    CK(hipMalloc(&c.rowb, dvc::CclBufs::rowb_bytes(g, n)));
     c.stats = stats;
     const int B = 4, NBX = (W + B - 1) / B, NBY = (H + B - 1) / B, SW = (NBX + 63) / 64, gs = (W + 3) & ~3;
     uint64_t *dblk, *rblk, *sbits;
@@ -114,7 +115,7 @@ int main(int argc, char** argv)
         auto t0 = std::chrono::steady_clock::now();
         // rep 0 starts from the 25x25-blurred prime gray (a near-full first mask);
         // later reps continue from the previous rep's last gray like a feed would
-        CK(dvc::launch_front(frames + F, 3 * W, F, n, (r & 1) ? gray1 : gray0, (r & 1) ? gray0 : gray1, gs, c.mbits, g,
+        CK(dvc::launch_front(frames + F, 3 * W, F, dvc::SrcFmt{0, 0, 0, 0}, n, (r & 1) ? gray1 : gray0, (r & 1) ? gray0 : gray1, gs, c.mbits, g,
                              0, nullptr));
         CK(hipDeviceSynchronize());
         auto t1 = std::chrono::steady_clock::now();
