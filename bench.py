@@ -24,10 +24,17 @@ instead).
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
 
+Timing: ``--runs`` (5) timed runs of exactly ``--steps`` steps each, each
+bracketed by a barrier and a device sync; ``value`` is the median run (max over
+ranks per run), every run's value under ``timing``. ``ranks`` records the
+world size the process group saw and every rank's own frame count.
+
 Extra JSON fields: ``roofline`` for the dominant kernel (k_out: hipEvent time
-per launch on the back stream, in a second pass of the same steps) and
+per launch on the back stream, in a second pass of the same steps; ``copy``:
+the same bytes against this box's hand-written copy rate, dvc_copy_rate) and
 ``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
-feed; rank 0 at N=1 only).
+feed, with ``all_cores``: one feed per available core up to the box's CPU
+share; rank 0 at N=1 only).
 
 ``--path of`` runs the fused optical-flow worker of motion_compression_opt.py
 (of:65-101 + of:141-185: gray, Farneback 3-level pyramid, vote, close/open,
@@ -134,25 +141,16 @@ def cpu_baseline(width: int, height: int, budget_s: float, max_frames: int, path
                       f"synthetic workload (seeds 0..{len(jobs) - 1}), {nf} frames in {secs:.1f} s"}
 
 
-def copy_bandwidth(dev, nbytes=1 << 30, reps=10):
-    """This GPU's device-to-device copy rate in GB/s (bytes read + written), the
+def copy_bandwidth(local: int, nbytes=2 << 30, reps=20):
+    """This GPU's streaming-copy rate in GB/s (bytes read + written), the
     practical ceiling SURVEY.md §8d asks the roofline to be quoted against
-    beside the 8 TB/s spec: one 1 GiB buffer copied `reps` times, event-timed."""
-    import torch
-    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    e1.synchronize()
-    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+    beside the 8 TB/s spec: dvc_copy_rate, a hand-written 16-B-per-lane copy
+    (the form MI355X_MICROARCH.md measures 6.29 TB/s with) of a 2 GiB buffer,
+    with plain and with nontemporal stores; the faster of the two."""
+    import dvc_amd
+    plain = dvc_amd._native.copy_rate(local, nbytes, reps, nontemporal=False)
+    nt = dvc_amd._native.copy_rate(local, nbytes, reps, nontemporal=True)
+    return max(plain, nt), {"plain_stores": round(plain, 1), "nontemporal_stores": round(nt, 1)}
 
 
 def main():
@@ -188,8 +186,11 @@ def main():
     ap.add_argument("--out-format", choices=("BGR", "I420"), default="BGR",
                     help="FD outputs as the encoder's 4:2:0 input (cvtColor BGR2YUV_I420 of the frames fd:112,131 "
                          "hand to VideoWriter; DVC_FLAG_OUT_I420) instead of BGR")
-    ap.add_argument("--cpu-cores", type=int, default=1,
-                    help="CPU baseline: this many feeds on this many host processes (1 = single core)")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="CPU baseline's multi-core leg: this many feeds on this many host processes (0: every "
+                         "available CPU up to the box's CPU share, DVC_CPU_SHARE, default 16)")
+    ap.add_argument("--runs", type=int, default=5,
+                    help="timed runs of --steps steps each; the line reports the median run (SURVEY.md §8d)")
     args = ap.parse_args()
 
     import numpy as np
@@ -317,13 +318,19 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    run_steps(ws, args.steps)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
+    # --runs timed runs of exactly --steps steps each, every one bracketed by a
+    # barrier + device sync on both sides; the line reports the median run
+    # (max over ranks per run), all runs listed beside it
+    runs = max(1, args.runs)
+    elapsed_runs = []
+    for _ in range(runs):
+        barrier()
+        t0 = time.perf_counter()
+        run_steps(ws, args.steps)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        barrier()
+        elapsed_runs.append(t1 - t0)
     sts = [w.stats() for w in ws]
     st = {k: sum(x[k] for x in sts) for k in sts[0]}
     for w in ws:
@@ -340,14 +347,22 @@ def main():
     wk.close()
     kframes = ksteps * P
 
-    vec = torch.tensor([elapsed, st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
-                       dtype=torch.float64, device="cpu" if one_dev else dev)
+    red_dev = "cpu" if one_dev else dev
+    vec = torch.tensor([st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
+                       dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor(elapsed_runs, dtype=torch.float64, device=red_dev)
+    per_rank = torch.zeros(world, dtype=torch.float64, device=red_dev)
+    per_rank[rank] = st["frames"]
+    ranks = {"world_size": 1, "backend": None, "frames_per_rank": [int(st["frames"])]}
     if world > 1:
-        tmax = vec[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM)   # RCCL: end-of-run aggregate stats only
-        vec[0] = tmax[0]
-    elapsed_max = float(vec[0])
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)       # per run: the slowest rank's time
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)        # RCCL: end-of-run aggregate stats only
+        dist.all_reduce(per_rank, op=dist.ReduceOp.SUM)   # each rank's own frame count
+        ranks = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                 "frames_per_rank": [int(x) for x in per_rank.tolist()]}
+    run_times = sorted(float(x) for x in tmax.tolist())
+    elapsed_max = run_times[len(run_times) // 2] if len(run_times) % 2 else \
+        0.5 * (run_times[len(run_times) // 2 - 1] + run_times[len(run_times) // 2])
     frames_total = args.steps * P * F * world
     value = frames_total * W * H / elapsed_max / 1e6
 
@@ -419,13 +434,22 @@ def main():
                          "frames_per_launch": round(per_launch_frames, 2),
                          "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn,
                          "timed_with": "feed 0 alone"},
-            "stats": {"frames": int(vec[1]), "motion_px": int(vec[2]), "components": int(vec[3]),
-                      "static_blocks": int(vec[4])},
+            "stats": {"frames": int(vec[0]), "motion_px": int(vec[1]), "components": int(vec[2]),
+                      "static_blocks": int(vec[3])},
+            "timing": {"runs": runs, "reported": "median run", "steps_per_run": args.steps,
+                       "value_per_run": [round(frames_total * W * H / t / 1e6, 2) for t in
+                                         (float(x) for x in tmax.tolist())]},
+            "ranks": ranks,
         }
+        if traffic is not None:
+            line["roofline"]["traffic_source"] = (
+                "committed rocprofv3 PMC profile of the same workload and launch size (2 x FETCH_SIZE + "
+                "WRITE_SIZE, tools/profile_round.sh): profiles/" + ("pmc_summary_of.json" if of else "pmc_summary.json"))
         # the same kernel's bytes (and the pipeline's) against this box's measured copy rate
-        cp_gbs = copy_bandwidth(dev)
+        cp_gbs, cp_detail = copy_bandwidth(local)
         line["roofline"]["copy"] = {"GBps": round(cp_gbs, 1), "frac": round(achieved / cp_gbs, 4),
-                                    "pipeline_frac": round(line["config"]["pipeline_GBps_per_gpu"] / cp_gbs, 4)}
+                                    "pipeline_frac": round(line["config"]["pipeline_GBps_per_gpu"] / cp_gbs, 4),
+                                    "kernel": "dvc_copy_rate: hand-written 16 B/lane copy of 2 GiB", **cp_detail}
         if of:   # k_flow's binding axis is the VALU (serial f64 recurrences), not HBM
             px_it = W * H * per_launch_frames
             flops = px_it * (OF_FLOW_F32_FLOPS_PER_PX + 2 * OF_FLOW_F64_FLOPS_PER_PX)
@@ -444,7 +468,21 @@ def main():
                                         "frac": hbm["frac"], "copy": hbm.get("copy"),
                                         "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"]}}
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(W, H, args.cpu_budget, 120, args.path, args.cpu_cores)
+            # one host core (the oracle is single-threaded per feed), and beside it
+            # every available core up to the box's CPU share, one feed per core
+            base = cpu_baseline(W, H, args.cpu_budget, 120, args.path, 1)
+            try:
+                avail = len(os.sched_getaffinity(0))
+            except Exception:
+                avail = os.cpu_count() or 1
+            share = int(os.environ.get("DVC_CPU_SHARE", "16"))
+            ncores = args.cpu_cores or max(1, min(avail, share))
+            if ncores > 1:
+                mc = cpu_baseline(W, H, args.cpu_budget, 120, args.path, ncores)
+                mc["cap"] = (f"{ncores} of {avail} available CPUs: the GPU box's CPU share per GPU is {share} "
+                             f"(DVC_CPU_SHARE)") if ncores < avail else "every available CPU"
+                base["all_cores"] = mc
+            line["cpu_baseline"] = base
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

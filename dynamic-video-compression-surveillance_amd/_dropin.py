@@ -9,11 +9,23 @@ c+1 and writing chunk c-1 overlap chunk c's step instead of adding to it.
 Three buffers each way; file I/O, frame copies and the ctypes calls release
 the GIL. An input chunk is recycled after the writer is done with it (the
 OF driver writes the input frames as its overlay video).
+
+Per-frame time (``frame_times``): the reference times each frame from its
+``cap.read()`` to its last ``write`` (``frame_differencing.py:86,135``); its loop
+is sequential, so that interval is also the time the frame adds to the run and
+the per-frame times sum to the loop's wall time. The pipeline keeps that
+second meaning: a frame's time is the wall-clock interval between the write
+completion of the frame before it and its own (the first frame's starts at the
+pipeline's first read), spread evenly over the frames of a chunk. So
+frames x average = the loop's wall time <= the run's total time, as in the
+reference; a frame's read-to-write latency inside the pipeline (about three
+chunk periods) is not what the file reports.
 """
 from __future__ import annotations
 
 import queue
 import threading
+import time
 
 from ._native import pinned
 
@@ -25,10 +37,17 @@ class ChunkPipeline:
         """``read()`` -> (ok, frame) (cap.read); ``emit(i, outs, done, failing)``
         writes the first ``done`` frames of input chunk ``i`` / output buffers
         ``outs`` (on the writer thread). ``alloc(shape)``: the buffers, default
-        page-locked uint8 arrays (``_native.pinned``)."""
+        page-locked uint8 arrays (``_native.pinned``). ``in_shape`` may be a
+        list of shapes: then ``read()`` returns (ok, (frame_a, frame_b, ..)) —
+        several videos read in lockstep (compress_with_motion, of:142-143) —
+        and ``ins[i]`` is a tuple of chunk arrays."""
         self.R, self.read, self.emit = R, read, emit
         alloc = alloc or pinned
-        self.ins = [alloc((R,) + tuple(in_shape)) for _ in range(self.NBUF)]
+        self.multi = isinstance(in_shape, list)
+        shapes = in_shape if self.multi else [in_shape]
+        self.ins = [tuple(alloc((R,) + tuple(sh)) for sh in shapes) for _ in range(self.NBUF)]
+        if not self.multi:
+            self.ins = [x[0] for x in self.ins]
         self.outs = [tuple(alloc((R,) + tuple(s)) for s in out_shapes) for _ in range(self.NBUF)]
         self.free_in, self.free_out = queue.Queue(), queue.Queue()
         for k in range(self.NBUF):
@@ -38,8 +57,11 @@ class ChunkPipeline:
         self.error = None
         self._stop = threading.Event()
         self.reader = self.writer = None
+        self.t0 = None
+        self.departures = []             # (time the chunk's last write returned, frames in it)
 
     def start(self):
+        self.t0 = time.time()
         self.reader = threading.Thread(target=self._read_loop, name="dvc-reader", daemon=True)
         self.writer = threading.Thread(target=self._write_loop, name="dvc-writer", daemon=True)
         self.reader.start()
@@ -57,7 +79,11 @@ class ChunkPipeline:
                     ok, f = self.read()
                     if not ok:
                         break
-                    self.ins[i][n] = f
+                    if self.multi:
+                        for buf, x in zip(self.ins[i], f):
+                            buf[n] = x
+                    else:
+                        self.ins[i][n] = f
                     n += 1
                 self.filled.put((i, n))
                 if n < self.R:           # end of the video
@@ -74,6 +100,7 @@ class ChunkPipeline:
                     return
                 i, j, done, failing = item
                 self.emit(i, self.outs[j], done, failing)
+                self.departures.append((time.time(), done))
                 self.free_out.put(j)
                 self.free_in.put(i)
         except Exception as e:           # surfaced by next_chunk / out_buffer / finish
@@ -104,6 +131,16 @@ class ChunkPipeline:
         self.writer.join()
         if self.error is not None:
             raise self.error
+
+    def frame_times(self):
+        """Seconds per written frame (module docstring): chunk c's frames share
+        the interval since chunk c-1's writes completed."""
+        out, prev = [], self.t0
+        for t, done in self.departures:
+            if done > 0:
+                out.extend([(t - prev) / done] * done)
+                prev = t
+        return out
 
     def stop(self):
         self._stop.set()

@@ -16,7 +16,7 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libdvc_hip.so")
-SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip", "yuv_kernels.hip"]
+SOURCES = ["fd_kernels.hip", "fd_api.hip", "of_kernels.hip", "of_api.hip", "yuv_kernels.hip", "diag.hip"]
 HEADERS = ["fd_kernels.h", "dvc_device.h", "of_kernels.h", "host_common.h", "yuv_kernels.h", "yuv_px.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
@@ -43,8 +43,9 @@ EXPORTS = [
     "dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync", "dvc_of_get_stats",
     "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
     "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free", "dvc_yuv420_to_bgr", "dvc_bgr_to_i420",
+    "dvc_copy_rate", "dvc_ofc_create", "dvc_ofc_run", "dvc_ofc_sync", "dvc_ofc_destroy",
 ]
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_BATCH = 512
 
 
@@ -190,6 +191,15 @@ def lib() -> ctypes.CDLL:
     L.dvc_of_destroy.restype = None
     L.dvc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                   u8p]
+    L.dvc_ofc_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, vp,
+                                 ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.dvc_ofc_run.argtypes = [vp, u8p, ctypes.c_size_t, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_size_t,
+                              ctypes.c_int, ctypes.c_int, u8p, ctypes.c_size_t]
+    L.dvc_ofc_sync.argtypes = [vp]
+    L.dvc_ofc_destroy.argtypes = [vp]
+    L.dvc_ofc_destroy.restype = None
+    for name in ("dvc_ofc_create", "dvc_ofc_run", "dvc_ofc_sync"):
+        getattr(L, name).restype = ctypes.c_int
     L.dvc_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(vp)]
     L.dvc_host_alloc.restype = ctypes.c_int
     L.dvc_host_free.argtypes = [vp]
@@ -200,6 +210,9 @@ def lib() -> ctypes.CDLL:
     L.dvc_bgr_to_i420.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, vp,
                                   ctypes.c_uint32]
+    L.dvc_copy_rate.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_double)]
+    L.dvc_copy_rate.restype = ctypes.c_int
     L.dvc_yuv420_to_bgr.restype = ctypes.c_int
     L.dvc_bgr_to_i420.restype = ctypes.c_int
     for name in ("dvc_of_create", "dvc_of_prime", "dvc_of_step", "dvc_of_step_batch", "dvc_of_sync",
@@ -274,6 +287,47 @@ def of_compress(bgr, mask, quant: float = 100.0, device: int = 0):
     return out
 
 
+class OFCompressor:
+    """compress_with_motion's loop (of:141-185) on the GPU for chunks of frames
+    (dvc_ofc): host numpy frames (n, H, W, 3) and decoded masks (n, H, W) or
+    (n, H, W, 3) -> compressed frames (n, H, W, 3)."""
+
+    def __init__(self, width: int, height: int, quant: float = 100.0, max_batch: int = 32, device: int = 0):
+        self.W, self.H, self.max_batch = int(width), int(height), max(1, int(max_batch))
+        h = ctypes.c_void_p()
+        check(lib().dvc_ofc_create(self.W, self.H, float(quant), self.max_batch, int(device), None, 0,
+                                   ctypes.byref(h)))
+        self._h = h
+
+    def run(self, frames, masks, out=None):
+        import numpy as np
+        f = np.ascontiguousarray(frames, dtype=np.uint8)
+        m = np.ascontiguousarray(masks, dtype=np.uint8)
+        if f.ndim == 3:
+            f, m = f[None], m[None]
+        n = f.shape[0]
+        ch = 3 if m.ndim == 4 else 1
+        if f.shape[1:] != (self.H, self.W, 3) or m.shape[:3] != (n, self.H, self.W):
+            raise ValueError(f"frames {f.shape} / masks {m.shape} do not match {self.W}x{self.H}")
+        if out is None:
+            out = np.empty_like(f)
+        if n:
+            check(lib().dvc_ofc_run(self._h, f.ctypes.data, 3 * self.W, f[0].nbytes, m.ctypes.data, self.W * ch,
+                                    m[0].nbytes, ch, n, out.ctypes.data, out[0].nbytes))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dvc_ofc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def yuv420_to_bgr(frames, fmt: str = "I420", device: int = 0):
     """cv2.cvtColor(COLOR_YUV2BGR_I420 / _NV12) on the GPU of host 4:2:0 frames:
     one (H*3/2, W) uint8 frame or an (n, H*3/2, W) stack -> (.., H, W, 3) BGR."""
@@ -304,6 +358,14 @@ def bgr_to_i420(frames, device: int = 0):
     check(lib().dvc_bgr_to_i420(f.ctypes.data, 3 * W, 3 * W * H, W, H, n, out.ctypes.data, W, 0, out[0].nbytes,
                                 int(device), None, 0))
     return out[0] if one else out
+
+
+def copy_rate(device: int = 0, nbytes: int = 1 << 30, reps: int = 20, nontemporal: bool = True) -> float:
+    """dvc_copy_rate: this GPU's hand-written streaming-copy rate in GB/s (bytes
+    read + written), the practical HBM ceiling the bench quotes beside 8 TB/s."""
+    g = ctypes.c_double()
+    check(lib().dvc_copy_rate(int(device), int(nbytes), int(reps), int(bool(nontemporal)), ctypes.byref(g)))
+    return g.value
 
 
 def gaussian_taps_q8(n: int, sigma: float) -> list:

@@ -473,24 +473,20 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame
     for (int k = 0; k < NSLOT; ++k) {
         Slot& s = h->slot[k];
-        size_t sz[10];
+        size_t sz[dvc::CclBufs::NARR];
         dvc::CclBufs::sizes(h->g, mb, sz);
-        void** ptrs[10] = {(void**)&s.c.mbits, (void**)&s.c.fbits, (void**)&s.c.rs, (void**)&s.c.re,
-                           (void**)&s.c.nfg, (void**)&s.c.fpar, (void**)&s.c.gpar, (void**)&s.c.gE,
-                           (void**)&s.c.area2, (void**)&s.c.kbits};
+        void** ptrs[dvc::CclBufs::NARR];
+        s.c.ptrs(ptrs);
         // Only the motion bits (written by the front of a later batch while this
         // one's contour filter runs) and the kept bits (read by the accumulate
         // stage after it) belong to a slot; the filter's run index, parents,
-        // areas and filled bits (indices 1..8, ~17 MB per 1080p frame) are
-        // touched only inside the contour-filter stage, whose batches run one
-        // after another on the handle's stream: one set serves all slots.
-        for (int i = 0; i < 10; ++i) {
-            const bool shared = i >= 1 && i <= 8;
-            if (shared && k > 0) continue;   // slot 0's, set below
+        // areas and filled bits (~17 MB per 1080p frame) are touched only
+        // inside the contour-filter stage, whose batches run one after another
+        // on the handle's stream: one set serves all slots.
+        for (int i = 0; i < dvc::CclBufs::NARR; ++i) {
+            if (dvc::CclBufs::working_set(i) && k > 0) continue;   // slot 0's, set below
             if ((e = dalloc(ptrs[i], sz[i])) != hipSuccess) return bad(e, "hipMalloc");
         }
-        if (k == 0 && (e = dalloc(&s.c.rowb, dvc::CclBufs::rowb_bytes(h->g, mb))) != hipSuccess)
-            return bad(e, "hipMalloc");
         if (k > 0) {
             const dvc::CclBufs& c0 = h->slot[0].c;
             s.c.rowb = c0.rowb;
@@ -589,7 +585,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     // the OUTSIDE gap node of every frame slice is its own root before any
     // k_band runs (its over-budget path may walk through it)
     {
-        size_t sz[10];
+        size_t sz[dvc::CclBufs::NARR];
         dvc::CclBufs::sizes(h->g, mb, sz);
         if ((e = hipMemsetAsync(h->slot[0].c.gpar, 0, sz[6], h->stream)) != hipSuccess) return bad(e, "hipMemset");
     }
@@ -1028,46 +1024,45 @@ int dvc_contour_filter(const uint8_t* mask, int width, int height, int64_t min_a
         return fail(DVC_E_INVALID, "mask %dx%d: sides must be 4..65520", width, height);
     HIP_OK(hipSetDevice(device));
     dvc::RowGeom g{width, height, (width + 63) / 64, width / 2 + 1};
-    const size_t W = width, H = height, N = W * H, WW = g.WW, CAP = g.CAP;
+    const size_t W = width, H = height, WW = g.WW;
     std::vector<uint64_t> bits(H * WW, 0);
     for (size_t y = 0; y < H; ++y)
         for (size_t x = 0; x < W; ++x)
             if (mask[y * W + x]) bits[y * WW + x / 64] |= 1ull << (x % 64);
+    dvc::CclBufs c{};
+    size_t sz[dvc::CclBufs::NARR];
+    void** ptrs[dvc::CclBufs::NARR];
+    dvc::CclBufs::sizes(g, 1, sz);
+    c.ptrs(ptrs);
+    unsigned long long* stats = nullptr;
     std::vector<void*> owned;
-    auto alloc = [&](size_t bytes) -> void* {
-        void* p = nullptr;
-        if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
-        owned.push_back(p);
-        return p;
+    bool oom = false;   // every allocation is checked before any launch
+    auto alloc = [&](void** p, size_t bytes) {
+        *p = nullptr;
+        if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
+            *p = nullptr;
+            oom = true;
+            return;
+        }
+        owned.push_back(*p);
     };
-    uint64_t* mbits = (uint64_t*)alloc(8 * H * WW);
-    uint64_t* fbits = (uint64_t*)alloc(8 * H * WW);
-    uint64_t* kept = (uint64_t*)alloc(8 * H * WW);
-    uint16_t* rs = (uint16_t*)alloc(2 * H * CAP);
-    uint16_t* re = (uint16_t*)alloc(2 * H * CAP);
-    uint32_t* nfg = (uint32_t*)alloc(4 * H);
-    uint32_t* fpar = (uint32_t*)alloc(4 * H * CAP);
-    uint32_t* gpar = (uint32_t*)alloc(4 * (1 + H * (CAP + 1)));
-    uint8_t* gE = (uint8_t*)alloc(H * (CAP + 1));
-    uint32_t* area2 = (uint32_t*)alloc(4 * H * CAP);
-    uint32_t* rowb = (uint32_t*)alloc(8 * H);
-    unsigned long long* stats = (unsigned long long*)alloc(8 * 4 * 64);
+    for (int i = 0; i < dvc::CclBufs::NARR; ++i) alloc(ptrs[i], sz[i]);
+    alloc((void**)&stats, 8 * 4 * 64);
+    c.stats = stats;
     int rc = DVC_OK;
     auto done = [&]() { for (void* p : owned) (void)hipFree(p); };
-    for (void* p : owned)
-        if (!p) { done(); return fail(DVC_E_NOMEM, "hipMalloc failed"); }
-    hipStream_t s = nullptr;
-    hipError_t e = hipMemcpy(mbits, bits.data(), 8 * H * WW, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(stats, 0, 8 * 4 * 64);
-    if (e == hipSuccess) e = hipMemset(gpar, 0, 4 * (1 + H * (CAP + 1)));
-    if (e == hipSuccess) {
-        dvc::CclBufs c{mbits, fbits, rs, re, nfg, fpar, gpar, gE, area2, kept, stats};
-        c.rowb = rowb;
-        e = dvc::launch_ccl(c, g, 1, min_area2, s);
+    if (oom) {
+        done();
+        return fail(DVC_E_NOMEM, "hipMalloc failed");
     }
+    hipStream_t s = nullptr;
+    hipError_t e = hipMemcpy(c.mbits, bits.data(), 8 * H * WW, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(stats, 0, 8 * 4 * 64);
+    if (e == hipSuccess) e = hipMemset(c.gpar, 0, sz[6]);
+    if (e == hipSuccess) e = dvc::launch_ccl(c, g, 1, min_area2, s);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     unsigned long long st[4] = {0, 0, 0, 0}, slots[64 * 4];
-    if (e == hipSuccess) e = hipMemcpy(bits.data(), kept, 8 * H * WW, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(bits.data(), c.kbits, 8 * H * WW, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(slots, stats, sizeof(slots), hipMemcpyDeviceToHost);
     for (int i = 0; i < 64 * 4; ++i) st[i % 4] += slots[i];
     if (e != hipSuccess) rc = fail(DVC_E_HIP, "contour filter: %s", hipGetErrorString(e));

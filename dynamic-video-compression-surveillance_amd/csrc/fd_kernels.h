@@ -65,13 +65,26 @@ struct CclBufs {
                        gpar + f * (ng + 1), gE + f * ng, area2 + f * nr, kbits + f * nb, stats,
                        kocc ? kocc + f * g.H : nullptr, kfull, rowb + f * 2 * g.H};
     }
-    // bytes of every array for `frames` frames (host allocation)
-    static void sizes(const RowGeom& g, size_t frames, size_t out[10])
+    // Bytes of every array for `frames` frames (host allocation), in the order
+    // of ptrs(): a caller that allocates these NARR arrays has every buffer the
+    // kernels touch (launch_ccl refuses a CclBufs without rowb).
+    static constexpr int NARR = 11;
+    static void sizes(const RowGeom& g, size_t frames, size_t out[NARR])
     {
         const size_t nb = (size_t)g.H * g.WW, nr = (size_t)g.H * g.CAP, ng = (size_t)g.H * (g.CAP + 1);
-        const size_t s[10] = {8 * nb, 8 * nb, 2 * nr, 2 * nr, 4 * (size_t)g.H, 4 * nr, 4 * (ng + 1), ng, 4 * nr, 8 * nb};
-        for (int i = 0; i < 10; ++i) out[i] = s[i] * frames;
+        const size_t s[NARR] = {8 * nb, 8 * nb, 2 * nr, 2 * nr, 4 * (size_t)g.H, 4 * nr, 4 * (ng + 1), ng, 4 * nr, 8 * nb,
+                                rowb_bytes(g, 1)};
+        for (int i = 0; i < NARR; ++i) out[i] = s[i] * frames;
     }
+    // the arrays sizes() describes; indices 1..8 and 10 are contour-filter
+    // working set (touched only inside launch_ccl), 0 and 9 its input / output
+    void ptrs(void** out[NARR])
+    {
+        void** p[NARR] = {(void**)&mbits, (void**)&fbits, (void**)&rs,    (void**)&re,    (void**)&nfg, (void**)&fpar,
+                          (void**)&gpar,  (void**)&gE,    (void**)&area2, (void**)&kbits, (void**)&rowb};
+        for (int i = 0; i < NARR; ++i) out[i] = p[i];
+    }
+    static bool working_set(int i) { return (i >= 1 && i <= 8) || i == 10; }
 };
 
 // The frames k_front / k_out / k_out_gen read: packed BGR rows (fmt 0,

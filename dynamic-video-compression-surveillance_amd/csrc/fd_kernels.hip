@@ -1534,6 +1534,7 @@ static int band_budget(const RowGeom& g)
 
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s)
 {
+    if (!c.rowb) return hipErrorInvalidValue;   // every kernel below finds its nodes through rowb
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
     hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(256), band_lds(g, BH, budget), s, c, g, budget);
     if (nb > 1)

@@ -105,6 +105,27 @@ void lin_taps(int sw, int dw, std::vector<dvc::LinTap>& out)
     }
 }
 
+// getStructuringElement(MORPH_ELLIPSE, (k, k)) (of:62; oc_ellipse_element) as
+// per-row column ranges relative to the anchor (k/2, k/2): row i covers
+// dx = mlo[i] .. mhi[i] (mlo > mhi: empty row).
+void ellipse_rows(int k, dvc::OfGeom& g)
+{
+    const int r = k / 2, c = k / 2;
+    const double inv_r2 = r ? 1. / ((double)r * r) : 0;
+    g.mk = k;
+    for (int i = 0; i < k; ++i) {
+        const int dy = i - r;
+        int j1 = 0, j2 = 0;
+        if (std::abs(dy) <= r) {
+            const int dx = (int)std::lrint(c * std::sqrt((r * r - dy * dy) * inv_r2));
+            j1 = std::max(c - dx, 0);
+            j2 = std::min(c + dx + 1, k);
+        }
+        g.mlo[i] = (int8_t)(j1 < j2 ? j1 - c : 1);
+        g.mhi[i] = (int8_t)(j1 < j2 ? j2 - 1 - c : 0);
+    }
+}
+
 // smallest c with c*255 >= alpha*L*255 in float64 (of:86; oc_vote_threshold)
 int vote_threshold(double alpha, int L)
 {
@@ -120,8 +141,9 @@ int vote_threshold(double alpha, int L)
 struct OfSlot {
     hipEvent_t ev_pyr = nullptr, ev_flow = nullptr, ev_mask = nullptr;
     bool recorded = false;
-    uint8_t* fin = nullptr;   // YUV input: the batch's frames converted to BGR (pitch 3W), read by
-                              // the pyramid and by k_of_out
+    uint8_t* fin = nullptr;   // staged input: YUV frames converted to BGR, or BGR frames the kernels
+                              // cannot read in place, re-pitched (rows of ip), read by the pyramid
+                              // and by k_of_out
 };
 
 struct dvc_of {
@@ -141,6 +163,7 @@ struct dvc_of {
     dvc::OfBufs b{};
     dvc::DctMat M{};
     int max_batch = 1;
+    int ip = 0;                          // row pitch the kernels read BGR frames with: 3 * roundup(W, 4)
     int fmt = DVC_FMT_BGR, crows = 0;   // frame format handed to prime/step (DVC_FMT_*)
     long long a_next = 1;
     bool primed = false;
@@ -221,13 +244,51 @@ static hipError_t of_alloc(dvc_of* h, T** p, size_t bytes)
 
 extern "C" {
 
-// Frames handed to prime/step: BGR rows of `pitch` (>= 3W, % 4), or 4:2:0
+// Frames handed to prime/step: BGR rows of `pitch` (>= 3W), or 4:2:0
 // surfaces (luma pitch >= W; I420: even).
 static bool of_pitch_ok(const dvc_of* h, size_t pitch)
 {
     const size_t W = h->p.width;
-    if (h->fmt == DVC_FMT_BGR) return pitch >= 3 * W && pitch % 4 == 0;
+    if (h->fmt == DVC_FMT_BGR) return pitch >= 3 * W;
     return pitch >= W && (h->fmt != DVC_FMT_I420 || pitch % 2 == 0);
+}
+
+// Can the kernels read these BGR device frames in place? Dword rows reaching
+// whole 4-px quads (3 * roundup(W, 4) bytes), aligned base and frame stride;
+// anything else is re-pitched into the slot's staging frames first.
+static bool of_direct(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
+{
+    return pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
+}
+
+// The BGR frames the kernels read for a batch in slot S: the caller's device
+// frames in place, or (re-pitch needed, or 4:2:0 surfaces) converted / copied
+// into S.fin on stream `st` once the slot's previous batch is done with it.
+static int of_stage(dvc_of* h, OfSlot& S, const uint8_t* d, int dp, size_t fstride, int n, int crows, hipStream_t st,
+                    const uint8_t** kd, int* kp, size_t* kfs)
+{
+    const size_t W = h->p.width, H = h->p.height, FS = (size_t)h->ip * H;
+    if (h->fmt == DVC_FMT_BGR && of_direct(h, d, (size_t)dp, fstride, n)) {
+        *kd = d;
+        *kp = dp;
+        *kfs = fstride;
+        return DVC_OK;
+    }
+    if (!S.fin) HIP_OK(of_alloc(h, &S.fin, FS * h->max_batch));
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(st, S.ev_mask, 0));   // batch i-2's k_of_out read S.fin
+    if (h->fmt != DVC_FMT_BGR) {   // cvtColor of the decoded surfaces (what cap.read() returns, of:54,66)
+        HIP_OK(dvc::launch_yuv420_to_bgr(dvc::yuv_layout(d, dp, h->fmt, crows, fstride), (int)W, (int)H, n, S.fin,
+                                         h->ip, FS, st));
+    } else if (n == 1 || fstride == (size_t)dp * H) {
+        HIP_OK(hipMemcpy2DAsync(S.fin, h->ip, d, dp, 3 * W, H * n, hipMemcpyDeviceToDevice, st));
+    } else {
+        for (int t = 0; t < n; ++t)
+            HIP_OK(hipMemcpy2DAsync(S.fin + t * FS, h->ip, d + t * fstride, dp, 3 * W, H, hipMemcpyDeviceToDevice, st));
+    }
+    *kd = S.fin;
+    *kp = h->ip;
+    *kfs = FS;
+    return DVC_OK;
 }
 
 static size_t of_frame_span(const dvc_of* h, size_t pitch)
@@ -237,12 +298,12 @@ static size_t of_frame_span(const dvc_of* h, size_t pitch)
 }
 
 // A host frame into pinned staging in the layout the device copy is read with
-// (BGR rows of 3W; YUV: luma rows of W and the chroma plane(s) right after).
+// (BGR rows of ip; YUV: luma rows of W and the chroma plane(s) right after).
 static void of_pack_host(const dvc_of* h, const uint8_t* src, size_t pitch, uint8_t* dst)
 {
     const size_t W = h->p.width, H = h->p.height;
     if (h->fmt == DVC_FMT_BGR) {
-        for (size_t y = 0; y < H; ++y) std::memcpy(dst + y * 3 * W, src + y * pitch, 3 * W);
+        for (size_t y = 0; y < H; ++y) std::memcpy(dst + y * h->ip, src + y * pitch, 3 * W);
         return;
     }
     const dvc::YuvLayout L = dvc::yuv_layout(src, pitch, h->fmt, h->crows, 0);
@@ -261,9 +322,8 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     const dvc_of_params& p = *prm;
     if (p.width < 8 || p.height < 8 || p.width > 65520)
         return fail(DVC_E_INVALID, "frame %dx%d outside 8..65520 x >=8", p.width, p.height);
-    if (p.width % 8 || p.height % 8)
-        return fail(DVC_E_UNSUPPORTED, "frame %dx%d: the GPU path needs multiples of 8", p.width, p.height);
-    if (p.morph_kernel != 2) return fail(DVC_E_UNSUPPORTED, "morph_kernel %d: the GPU path implements 2", p.morph_kernel);
+    if (p.morph_kernel < 1 || p.morph_kernel > dvc::OF_MAX_MORPH)
+        return fail(DVC_E_UNSUPPORTED, "morph_kernel %d outside 1..%d", p.morph_kernel, dvc::OF_MAX_MORPH);
     if (p.window < 1 || p.window > 127) return fail(DVC_E_UNSUPPORTED, "window_size %d outside 1..127", p.window);
     if (p.poly_n != 5 && p.poly_n != 7) return fail(DVC_E_UNSUPPORTED, "poly_n %d: 5 or 7", p.poly_n);
     if (p.winsize < 1 || p.winsize / 2 > dvc::OF_MAX_BOX_M)
@@ -298,6 +358,8 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     dvc::OfGeom& g = h->g;
     g.W = p.width;
     g.H = p.height;
+    g.GP = (p.width + 3) & ~3;
+    h->ip = 3 * g.GP;
     g.WW = (p.width + 63) / 64;
     g.CAP = p.width / 2 + 1;
     g.L = L;
@@ -314,6 +376,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     g.sliding = !(p.flags & DVC_FLAG_OF_DIRECT_SUMS);
     poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
     dvc_host::dct_matrix(8, h->M);
+    ellipse_rows(p.morph_kernel, g);           // of:62
 
     auto bad = [&](hipError_t e, const char* what) {
         int rc = fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "%s: %s", what, hipGetErrorString(e));
@@ -402,7 +465,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     }
     dvc::OfBufs& b = h->b;
     struct { void** ptr; size_t bytes; } allocs[] = {
-        {(void**)&b.gray, N * mb},
+        {(void**)&b.gray, (size_t)g.GP * H * mb},
         {(void**)&b.mring, 8 * H * WW * g.RB},
         {(void**)&b.cnt, 64 * H * WW},
         {(void**)&b.vthr, 256},
@@ -443,14 +506,16 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     std::memset(vt, 0, sizeof(vt));
     for (int l = 1; l <= p.window; ++l) vt[l] = (uint8_t)vote_threshold(p.alpha_fraction, l);
     if ((e = hipMemcpy((void*)b.vthr, vt, 256, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
-    if (h->fmt != DVC_FMT_BGR)
+    const size_t FS = (size_t)h->ip * H;   // one staged / packed BGR frame
+    if (h->fmt != DVC_FMT_BGR)   // BGR device frames: allocated on first use (of_stage), when re-pitched
         for (OfSlot& sl : h->slot)
-            if ((e = of_alloc(h, &sl.fin, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
+            if ((e = of_alloc(h, &sl.fin, FS * mb)) != hipSuccess) return bad(e, "hipMalloc");
     if (!(p.flags & DVC_FLAG_DEVICE_PTRS)) {
-        if ((e = of_alloc(h, &h->d_in, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        const size_t FI = h->fmt == DVC_FMT_BGR ? FS : 3 * N;   // packed host frame (YUV: 1.5 N bytes used)
+        if ((e = of_alloc(h, &h->d_in, FI * mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = of_alloc(h, &h->d_mask, N * mb)) != hipSuccess) return bad(e, "hipMalloc");
         if ((e = of_alloc(h, &h->d_cp, 3 * N * mb)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = hipHostMalloc((void**)&h->h_in, 3 * N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
+        if ((e = hipHostMalloc((void**)&h->h_in, FI * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
         if ((e = hipHostMalloc((void**)&h->h_mask, N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
         if ((e = hipHostMalloc((void**)&h->h_cp, 3 * N * mb)) != hipSuccess) return bad(e, "hipHostMalloc");
     }
@@ -467,26 +532,30 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_sync_all(h));   // no batch of a previous run may still be in flight
     HIP_OK(of_wait_user(h));
-    const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW;
+    const size_t W = h->p.width, H = h->p.height, WW = h->g.WW;
     const uint8_t* d = bgr;
     int dp = (int)pitch, crows = h->crows;
     if (!(h->p.flags & DVC_FLAG_DEVICE_PTRS)) {
         of_pack_host(h, bgr, pitch, h->h_in);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, 3 * N, hipMemcpyHostToDevice, h->stream));
+        const size_t fb = h->fmt == DVC_FMT_BGR ? (size_t)h->ip * H : dvc::yuv_frame_bytes(W, (int)H);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, fb, hipMemcpyHostToDevice, h->stream));
         d = h->d_in;
-        dp = (int)(h->fmt == DVC_FMT_BGR ? 3 * W : W);
+        dp = (int)(h->fmt == DVC_FMT_BGR ? h->ip : W);
         crows = (int)H;
     }
-    if (h->fmt != DVC_FMT_BGR) {   // cvtColor of the decoded surface (what cap.read() returns, of:54)
-        HIP_OK(dvc::launch_yuv420_to_bgr(dvc::yuv_layout(d, dp, h->fmt, crows, 0), (int)W, (int)H, 1,
-                                         h->slot[0].fin, 3 * W, 3 * N, h->stream));
-        d = h->slot[0].fin;
-        dp = (int)(3 * W);
-    }
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, 3 * N, 0, 1, h->stream));   // of:60
+    for (OfSlot& sl : h->slot) sl.recorded = false;   // synced above: no batch in flight
+    const uint8_t* kd = nullptr;
+    int kp = 0;
+    size_t kfs = 0;
+    int rc = of_stage(h, h->slot[0], d, dp, 0, 1, crows, h->stream, &kd, &kp, &kfs);
+    if (rc) return rc;
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, kd, kp, kfs, 0, 1, h->stream));   // of:60
     HIP_OK(hipMemsetAsync(h->b.mring, 0, 8 * H * WW * h->g.RB, h->stream));            // of:61 deque()
     HIP_OK(hipMemsetAsync(h->b.cnt, 0, 64 * H * WW, h->stream));
     HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
+    // a new run: a hand-off timeout of an earlier run (reported by its sync)
+    // does not poison this one
+    HIP_OK(hipMemsetAsync(h->b.scan_abort, 0, 4, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
     for (OfSlot& sl : h->slot) sl.recorded = false;
     h->seq = 0;
@@ -518,16 +587,16 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
         return v;
     }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
-    if (h->fmt != DVC_FMT_BGR) {
-        // 4:2:0 surfaces -> BGR in the slot's frames (of:66,145), read by the
-        // pyramid and by k_of_out: batch i-2's k_of_out must be done with them
-        if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_mask, 0));
-        const size_t W = h->p.width, H = h->p.height;
-        HIP_OK(dvc::launch_yuv420_to_bgr(dvc::yuv_layout(d, dp, h->fmt, crows, fstride), (int)W, (int)H, n, S.fin,
-                                         3 * W, 3 * W * H, h->s_pyr));
-        d = S.fin;
-        dp = (int)(3 * W);
-        fstride = 3 * W * H;
+    {   // 4:2:0 surfaces -> BGR (of:66,145), or re-pitched BGR, in the slot's
+        // frames, read by the pyramid and by k_of_out
+        const uint8_t* kd = nullptr;
+        int kp = 0;
+        size_t kfs = 0;
+        int rc = of_stage(h, S, d, dp, fstride, n, crows, h->s_pyr, &kd, &kp, &kfs);
+        if (rc) return rc;
+        d = kd;
+        dp = kp;
+        fstride = kfs;
     }
     HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->s_pyr));
     HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
@@ -577,14 +646,12 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
     if (!h || !bgr) return fail(DVC_E_INVALID, "NULL argument");
     if (!h->primed) return fail(DVC_E_STATE, "step before dvc_of_prime");
     if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
-    const size_t W = h->p.width, H = h->p.height, N = W * H, row = 3 * W;
+    const size_t W = h->p.width, H = h->p.height, N = W * H;
     const bool yuv = h->fmt != DVC_FMT_BGR;
     if (!of_pitch_ok(h, pitch)) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    if (n > 1 && (fstride < of_frame_span(h, pitch) || (!yuv && fstride % 4)))
-        return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
-    if (n > 1 && mask && (mstride < N || mstride % 8)) return fail(DVC_E_INVALID, "mask stride %zu invalid", mstride);
-    if (n > 1 && compressed && (ostride < 3 * N || ostride % 4))
-        return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
+    if (n > 1 && fstride < of_frame_span(h, pitch)) return fail(DVC_E_INVALID, "frame stride %zu invalid", fstride);
+    if (n > 1 && mask && mstride < N) return fail(DVC_E_INVALID, "mask stride %zu invalid", mstride);
+    if (n > 1 && compressed && ostride < 3 * N) return fail(DVC_E_INVALID, "output frame stride %zu invalid", ostride);
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_wait_user(h));
     const bool devp = h->p.flags & DVC_FLAG_DEVICE_PTRS;
@@ -598,9 +665,10 @@ static int of_run(dvc_of* h, const uint8_t* bgr, size_t pitch, size_t fstride, i
             if (rc) return rc;
             continue;
         }
-        for (int t = 0; t < m; ++t) of_pack_host(h, in + (size_t)t * fstride, pitch, h->h_in + (size_t)t * 3 * N);
-        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * 3 * N, hipMemcpyHostToDevice, h->s_pyr));
-        int rc = of_enqueue(h, h->d_in, (int)(yuv ? W : row), 3 * N, m, mk ? h->d_mask : nullptr, N,
+        const size_t FI = yuv ? 3 * N : (size_t)h->ip * H;   // packed frame slot (of_pack_host)
+        for (int t = 0; t < m; ++t) of_pack_host(h, in + (size_t)t * fstride, pitch, h->h_in + (size_t)t * FI);
+        HIP_OK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)m * FI, hipMemcpyHostToDevice, h->s_pyr));
+        int rc = of_enqueue(h, h->d_in, (int)(yuv ? W : h->ip), FI, m, mk ? h->d_mask : nullptr, N,
                             cp ? h->d_cp : nullptr, 3 * N, (int)H);
         if (rc) return rc;
         if (mk) HIP_OK(hipMemcpyAsync(h->h_mask, h->d_mask, (size_t)m * N, hipMemcpyDeviceToHost, h->s_mask));
@@ -658,8 +726,9 @@ int dvc_of_read_plane(dvc_of* h, int plane, uint8_t* dst)
     HIP_OK(hipSetDevice(h->device));
     HIP_OK(of_sync_all(h));
     const size_t W = h->p.width, H = h->p.height, N = W * H, WW = h->g.WW, t = (size_t)h->last_n - 1;
-    if (plane == DVC_OF_PLANE_GRAY) {
-        HIP_OK(hipMemcpy(dst, h->b.gray + t * N, N, hipMemcpyDeviceToHost));
+    if (plane == DVC_OF_PLANE_GRAY) {   // rows of GP on the device
+        const size_t GP = h->g.GP;
+        HIP_OK(hipMemcpy2D(dst, W, h->b.gray + t * GP * H, GP, W, H, hipMemcpyDeviceToHost));
         return DVC_OK;
     }
     const uint64_t* src = nullptr;
@@ -743,53 +812,170 @@ void dvc_of_destroy(dvc_of* h)
     delete h;
 }
 
+}  // extern "C"
+
+// compress_with_motion (of:111-193) as a handle: the frames and decoded mask
+// frames of one video, n at a time. Device buffers for max_batch frames:
+// staged input frames (rows of ip), mask bits, outputs (host-pointer mode).
+struct dvc_ofc {
+    int W = 0, H = 0, WW = 0, ip = 0, device = 0, max_batch = 1;
+    uint32_t flags = 0;
+    float quant = 100.f;
+    hipStream_t stream = nullptr;    // the caller's (may be NULL = legacy default) or our own
+    bool own_stream = false;
+    uint8_t *fin = nullptr, *d_mask = nullptr, *d_out = nullptr;
+    uint64_t* bits = nullptr;
+    dvc::DctMat M{};
+};
+
+static void ofc_free(dvc_ofc* h)
+{
+    for (void* p : {(void*)h->fin, (void*)h->d_mask, (void*)h->d_out, (void*)h->bits})
+        if (p) (void)hipFree(p);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+extern "C" {
+
+int dvc_ofc_create(int width, int height, float quant, int max_batch, int device, void* hip_stream, uint32_t flags,
+                   dvc_ofc** out)
+{
+    if (!out) return fail(DVC_E_INVALID, "NULL argument");
+    if (width < 1 || height < 1 || width > 65520) return fail(DVC_E_INVALID, "frame %dx%d invalid", width, height);
+    if (!(quant == quant) || quant == 0.0f) return fail(DVC_E_INVALID, "quant must be nonzero");
+    if (max_batch < 0 || max_batch > DVC_MAX_BATCH) return fail(DVC_E_INVALID, "max_batch %d outside 1..%d", max_batch,
+                                                                DVC_MAX_BATCH);
+    HIP_OK(hipSetDevice(device));
+    dvc_ofc* h = new dvc_ofc();
+    h->W = width;
+    h->H = height;
+    h->WW = (width + 63) / 64;
+    h->ip = 3 * ((width + 3) & ~3);
+    h->device = device;
+    h->max_batch = max_batch ? max_batch : 1;
+    h->flags = flags;
+    h->quant = quant;
+    dvc_host::dct_matrix(8, h->M);
+    const size_t W = width, H = height, mb = h->max_batch;
+    hipError_t e = hipSuccess;
+    if (hip_stream) {
+        h->stream = (hipStream_t)hip_stream;
+    } else {
+        e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+        h->own_stream = e == hipSuccess;
+    }
+    if (e == hipSuccess) e = hipMalloc((void**)&h->bits, 8 * H * h->WW * mb);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->fin, (size_t)h->ip * H * mb);   // staged / re-pitched frames
+    if (e == hipSuccess && !(flags & DVC_FLAG_DEVICE_PTRS)) {
+        e = hipMalloc((void**)&h->d_mask, 3 * W * H * mb);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->d_out, 3 * W * H * mb);
+    }
+    if (e != hipSuccess) {
+        ofc_free(h);
+        delete h;
+        return fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "ofc create: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return DVC_OK;
+}
+
+int dvc_ofc_run(dvc_ofc* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, const uint8_t* mask,
+                size_t mask_pitch, size_t mask_stride, int mask_channels, int n, uint8_t* out, size_t out_stride)
+{
+    if (!h || !bgr || !mask || !out) return fail(DVC_E_INVALID, "NULL argument");
+    if (n < 0) return fail(DVC_E_INVALID, "negative frame count");
+    if (mask_channels != 1 && mask_channels != 3) return fail(DVC_E_INVALID, "mask_channels %d: 1 or 3", mask_channels);
+    const size_t W = h->W, H = h->H, N = W * H, FS = (size_t)h->ip * H;
+    if (pitch < 3 * W || mask_pitch < W * mask_channels) return fail(DVC_E_INVALID, "pitch invalid");
+    if (n > 1 && (frame_stride < pitch * (H - 1) + 3 * W || mask_stride < mask_pitch * (H - 1) + W * mask_channels ||
+                  out_stride < 3 * N))
+        return fail(DVC_E_INVALID, "frame / mask / output stride invalid");
+    HIP_OK(hipSetDevice(h->device));
+    const bool devp = h->flags & DVC_FLAG_DEVICE_PTRS;
+    hipStream_t st = h->stream;
+    dvc::OfGeom g{};
+    g.W = h->W;
+    g.H = h->H;
+    g.WW = h->WW;
+    g.GP = (h->W + 3) & ~3;
+    dvc::OfBufs b{};
+    for (int f0 = 0; f0 < n; f0 += h->max_batch) {
+        const int m = std::min(h->max_batch, n - f0);
+        const uint8_t* in = bgr + (size_t)f0 * frame_stride;
+        const uint8_t* mk = mask + (size_t)f0 * mask_stride;
+        uint8_t* o = out + (size_t)f0 * out_stride;
+        // frames the kernel reads: rows of pitch % 4 == 0 reaching whole quads
+        const uint8_t* kd = in;
+        size_t kp = pitch, kfs = frame_stride;
+        if (!devp || pitch % 4 || pitch < (size_t)h->ip || ((uintptr_t)in & 3) || (m > 1 && frame_stride % 4)) {
+            const hipMemcpyKind k = devp ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+            for (int t = 0; t < m; ++t)
+                HIP_OK(hipMemcpy2DAsync(h->fin + t * FS, h->ip, in + (size_t)t * frame_stride, pitch, 3 * W, H, k, st));
+            kd = h->fin;
+            kp = h->ip;
+            kfs = FS;
+        }
+        const uint8_t* dm = mk;
+        size_t dmp = mask_pitch, dms = mask_stride;
+        if (!devp) {   // decoded masks up (rows of W * channels)
+            const size_t mrow = W * mask_channels;
+            for (int t = 0; t < m; ++t)
+                HIP_OK(hipMemcpy2DAsync(h->d_mask + t * mrow * H, mrow, mk + (size_t)t * mask_stride, mask_pitch, mrow,
+                                        H, hipMemcpyHostToDevice, st));
+            dm = h->d_mask;
+            dmp = mrow;
+            dms = mrow * H;
+        }
+        HIP_OK(dvc::of_launch_mask_bits(dm, dmp, dms, mask_channels, h->W, h->H, m, h->bits, st));
+        dvc::OfOutArgs a{};
+        a.bgr = kd;
+        a.pitch = (int)kp;
+        a.fstride = kfs;
+        a.mbits = h->bits;
+        a.mbstride = H * h->WW;
+        a.compressed = devp ? o : h->d_out;
+        a.ostride = devp ? out_stride : 3 * N;
+        a.quant = h->quant;
+        a.qinv = 1.0 / (double)h->quant;
+        a.M = h->M;
+        HIP_OK(dvc::of_launch_out(g, b, a, m, st));
+        if (!devp) {
+            for (int t = 0; t < m; ++t)
+                HIP_OK(hipMemcpyAsync(o + (size_t)t * out_stride, h->d_out + t * 3 * N, 3 * N, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+        }
+    }
+    return DVC_OK;
+}
+
+int dvc_ofc_sync(dvc_ofc* h)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    return DVC_OK;
+}
+
+void dvc_ofc_destroy(dvc_ofc* h)
+{
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    ofc_free(h);
+    delete h;
+}
+
+// One frame, host pointers, synchronous: a one-frame dvc_ofc (any W, H; the
+// partial edge blocks are skipped as of:159,177 skip them).
 int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int width, int height, float quant,
                     int device, uint8_t* out)
 {
-    if (!bgr || !mask || !out) return fail(DVC_E_INVALID, "NULL argument");
-    if (width < 8 || height < 8 || width % 8 || height % 8)
-        return fail(DVC_E_UNSUPPORTED, "frame %dx%d: the GPU path needs multiples of 8", width, height);
-    if (pitch < 3 * (size_t)width || pitch % 4) return fail(DVC_E_INVALID, "pitch %zu invalid", pitch);
-    if (!(quant == quant) || quant == 0.0f) return fail(DVC_E_INVALID, "quant must be nonzero");
-    HIP_OK(hipSetDevice(device));
-    const size_t W = width, H = height, N = W * H, WW = (W + 63) / 64;
-    std::vector<uint64_t> bits(H * WW, 0);
-    for (size_t y = 0; y < H; ++y)
-        for (size_t x = 0; x < W; ++x)
-            if (mask[y * W + x]) bits[y * WW + x / 64] |= 1ull << (x % 64);
-    std::vector<uint8_t> in(3 * N);
-    for (size_t y = 0; y < H; ++y) std::memcpy(in.data() + y * 3 * W, bgr + y * pitch, 3 * W);
-    uint8_t *d_in = nullptr, *d_out = nullptr;
-    uint64_t* d_bits = nullptr;
-    hipError_t e = hipMalloc((void**)&d_in, 3 * N);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_out, 3 * N);
-    if (e == hipSuccess) e = hipMalloc((void**)&d_bits, 8 * H * WW);
-    if (e == hipSuccess) e = hipMemcpy(d_in, in.data(), 3 * N, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_bits, bits.data(), 8 * H * WW, hipMemcpyHostToDevice);
-    if (e == hipSuccess) {
-        dvc::OfGeom g{};
-        g.W = width;
-        g.H = height;
-        g.WW = (int)WW;
-        dvc::OfBufs b{};
-        b.rbits = d_bits;
-        dvc::OfOutArgs o{};
-        o.bgr = d_in;
-        o.pitch = 3 * width;
-        o.fstride = 3 * N;
-        o.compressed = d_out;
-        o.ostride = 3 * N;
-        o.quant = quant;
-        o.qinv = 1.0 / (double)quant;
-        dvc_host::dct_matrix(8, o.M);
-        e = dvc::of_launch_out(g, b, o, 1, nullptr);
-    }
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(out, d_out, 3 * N, hipMemcpyDeviceToHost);
-    for (void* p : {(void*)d_in, (void*)d_out, (void*)d_bits})
-        if (p) (void)hipFree(p);
-    if (e != hipSuccess) return fail(DVC_E_HIP, "of compress: %s", hipGetErrorString(e));
-    return DVC_OK;
+    dvc_ofc* h = nullptr;
+    int rc = dvc_ofc_create(width, height, quant, 1, device, nullptr, 0, &h);
+    if (rc) return rc;
+    rc = dvc_ofc_run(h, bgr, pitch, 0, mask, (size_t)width, 0, 1, 1, out, 0);
+    dvc_ofc_destroy(h);
+    return rc;
 }
 
 }  // extern "C"

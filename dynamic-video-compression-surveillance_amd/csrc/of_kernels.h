@@ -26,6 +26,7 @@ constexpr int OF_MAX_LEVELS = 6;
 constexpr int OF_MAX_POLY_N = 7;   // FarnebackPolyExp half-width n = poly_n (5 or 7)
 constexpr int OF_MAX_BOX_M = 8;    // winsize <= 17
 constexpr int OF_MAX_BLUR = 63;    // pyramid smoothing kernel taps
+constexpr int OF_MAX_MORPH = 31;   // morph_kernel (the ellipse's side, of:62)
 
 // FarnebackPrepareGaussian (optflowgf.cpp), n = poly_n: float taps, index k + n.
 struct PolyCoef {
@@ -57,6 +58,7 @@ struct Level {
 
 struct OfGeom {
     int W, H, WW, CAP;
+    int GP;            // row pitch of the gray frames: W rounded up to 4 (whole dword quads)
     int L;             // coarsest level index (levels L..0 are processed)
     int RS, RB;        // ring slots of R and of the raw motion bits
     int iters, m;      // Farneback iterations, box half-width (winsize / 2)
@@ -65,10 +67,15 @@ struct OfGeom {
     float flow_thr;
     int sliding;       // box sums in OpenCV's running order (k_flow_scan) / direct per pixel (k_flow)
     PolyCoef pc;
+    // getStructuringElement(MORPH_ELLIPSE, (mk, mk)) (of:62), anchor (mk/2, mk/2):
+    // element row i (dy = i - mk/2) covers dx = mlo[i] .. mhi[i] (empty if
+    // mlo > mhi); dilate / erode read src(x + dx, y + dy)
+    int mk;
+    int8_t mlo[OF_MAX_MORPH], mhi[OF_MAX_MORPH];
 };
 
 struct OfBufs {
-    uint8_t* gray;         // n x W*H, this batch's gray frames
+    uint8_t* gray;         // n x GP*H, this batch's gray frames (rows of GP)
     uint64_t* mring;       // RB x H*WW raw motion bits (|flow| > thr, of:82-83)
     uint32_t* cnt;         // H x WW*16 u32: vote counts, 4 px (bytes) per u32
     const uint8_t* vthr;   // vthr[L] = votes needed with L masks in the window (of:86), L <= window
@@ -94,11 +101,14 @@ struct OfBufs {
 };
 
 struct OfOutArgs {
-    const uint8_t* bgr;    // frame t at bgr + t*fstride, rows of `pitch` bytes
+    const uint8_t* bgr;    // frame t at bgr + t*fstride, rows of `pitch` bytes (pitch % 4 == 0 and
+                           // >= 3 * roundup(W, 4): whole dword quads are readable)
     int pitch;
     size_t fstride;
     uint8_t* mask;         // nullable: rectangle mask {0,255}, frame t at mask + t*mstride, rows of W
     size_t mstride;
+    const uint64_t* mbits; // nullable: the gating mask as bits (H x WW per frame at t*mbstride) instead
+    size_t mbstride;       //   of b.rbits (dvc_ofc: a decoded mask.mp4, of:141-149)
     uint8_t* compressed;   // nullable: frame t at compressed + t*ostride, rows of 3W
     size_t ostride;
     float quant;
@@ -120,5 +130,9 @@ inline int of_scan_strips(int w) { return (w + 31) / 32; }
 hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s);
 // compress_with_motion (of:151-183) + the mask bytes
 hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s);
+// a decoded mask plane (1 or 3 channels, rows of mpitch, frames of mstride) ->
+// nonzero-after-BGR2GRAY bits, H x WW words per frame (of:147-149)
+hipError_t of_launch_mask_bits(const uint8_t* mask, size_t mpitch, size_t mstride, int channels, int W, int H, int n,
+                               uint64_t* bits, hipStream_t s);
 
 }  // namespace dvc

@@ -163,17 +163,20 @@ __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, ui
     const int W = g.W, H = g.H;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     const uint8_t* f = bgr + (size_t)t * fstride;
-    uint8_t* go = gray_out + (size_t)t * W * H;
+    uint8_t* go = gray_out + (size_t)t * g.GP * H;
     for (int idx = tid; idx < GH * NQ; idx += 256) {
         const int i = idx / NQ, q = idx - i * NQ;
         const int y = y0 - HG + i, px = x0 - GX + 4 * q;
-        if (!INT && (y < 0 || y >= H || px < 0 || px >= W)) continue;   // W % 8 == 0: quads are whole
+        // the row's last quad may stick out past W: its bytes lie inside the row
+        // (pitch >= 3 * roundup(W, 4)), its gray values land in the gray rows'
+        // padding (GP) and in LDS columns the clamped / reflected taps never read
+        if (!INT && (y < 0 || y >= H || px < 0 || px >= W)) continue;
         const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)y * pitch + 3 * px);
         const uint32_t gq = gray4_dot(v.x, v.y, v.z);   // of:71 BGR2GRAY of 4 px
         *reinterpret_cast<float4*>(sg + i * GW + 4 * q) =
             make_float4((float)(gq & 255), (float)((gq >> 8) & 255), (float)((gq >> 16) & 255), (float)(gq >> 24));
         if (i >= HG && i < HG + PT_H && px >= x0 && px < x0 + PT_W)
-            *reinterpret_cast<uint32_t*>(go + (size_t)y * W + px) = gq;
+            *reinterpret_cast<uint32_t*>(go + (size_t)y * g.GP + px) = gq;
     }
     __syncthreads();
     // I = blur3(gray): horizontal pass at the 3 rows, then vertical (oc_blur_f32)
@@ -224,13 +227,13 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 // Horizontal smoothing pass (oc_blur_f32, first loop) of the full-resolution
 // gray at the 2w source columns the resize reads: tmpc[y][2dx] at xt[dx].s0,
 // tmpc[y][2dx+1] at xt[dx].s1. One workgroup per (row, frame), the gray row
-// staged in LDS (dynamic, W bytes; W % 8 == 0).
+// staged in LDS (dynamic, GP bytes: whole dwords).
 __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
 {
     extern __shared__ uint32_t srow[];
     const int y = blockIdx.x, t = blockIdx.y, W = g.W, H = g.H;
-    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(gray + (size_t)t * W * H + (size_t)y * W);
-    for (int i = threadIdx.x; i < W / 4; i += 256) srow[i] = s32[i];
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(gray + (size_t)t * g.GP * H + (size_t)y * g.GP);
+    for (int i = threadIdx.x; i < g.GP / 4; i += 256) srow[i] = s32[i];
     __syncthreads();
     const uint8_t* s = reinterpret_cast<const uint8_t*>(srow);
     const int r = lv.r, n2 = 2 * lv.w;
@@ -1084,14 +1087,32 @@ __global__ void __launch_bounds__(256) k_vote(OfGeom g, OfBufs b, long long a0, 
 
 // ---------------------------------------------------------- morphology + CCL
 // One workgroup per band of BH rows (one wave per row) of frame blockIdx.y.
-// MORPH_CLOSE then MORPH_OPEN with [[0,1],[1,1]] (anchor (1,1)): every pass
-// reads (x, y), (x-1, y), (x, y-1); out-of-image neighbours are ignored
-// (0 for dilate, 1 for erode). Four passes need 4 halo rows above the band.
-// Then the run index of each row, union-find of the band's runs (8-connected)
-// in LDS, band-local roots published as global ids (id = y*CAP + k), and
-// every run's bounding box initialised to itself.
-// Dynamic LDS: 2 x (BH+4) x WW u64 morph rows | run index (2 BH WW u64 +
-// 2 BH (WW+1) u16) | BH*CAP u32 parents.
+// MORPH_CLOSE then MORPH_OPEN with getStructuringElement(MORPH_ELLIPSE,
+// (mk, mk)) (of:62,89-90), anchor (a, a), a = mk/2: every pass reads
+// src(x + dx, y + dy) over the element's rows dy = -a .. mk-1-a and each row's
+// column range; out-of-image neighbours are ignored (0 for dilate, 1 for
+// erode). The reference's 2x2 element [[0,1],[1,1]] reads (x, y), (x-1, y),
+// (x, y-1) and takes a shift-and-OR form. Four passes need 4a halo rows above
+// the band and 4(mk-1-a) below. Then the run index of each row, union-find of
+// the band's runs (8-connected) in LDS, band-local roots published as global
+// ids (id = y*CAP + k), and every run's bounding box initialised to itself.
+// Dynamic LDS: 2 x NRW x WW u64 morph rows (NRW = BH + 4(mk-1)) | run index
+// (2 BH WW u64 + 2 BH (WW+1) u16) | BH*CAP u32 parents.
+
+// Bits [start, start + 64) of a mask row of WW words (W valid bits); positions
+// outside [0, W) read as `out` (all ones for erode, zeros for dilate).
+__device__ __forceinline__ uint64_t row_bits64(const uint64_t* row, int WW, uint64_t lastmask, int start, uint64_t out)
+{
+    const int w0 = start >> 6, sh = start & 63;   // arithmetic shift: floor for negative starts
+    auto word = [&](int i) -> uint64_t {
+        if (i < 0 || i >= WW) return out;
+        const uint64_t v = row[i];
+        return i == WW - 1 ? (v & lastmask) | (out & ~lastmask) : v;
+    };
+    const uint64_t lo = word(w0);
+    return sh ? (lo >> sh) | (word(w0 + 1) << (64 - sh)) : lo;
+}
+
 __global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
 {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -1100,7 +1121,8 @@ __global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
     const size_t plane = (size_t)H * WW, nr = (size_t)H * CAP;
     const uint64_t* sb = B.sbits + (size_t)t * plane;
     uint64_t* ob = B.obits + (size_t)t * plane;
-    const int NRW = BH + 4;
+    const int ma = g.mk / 2, mb = g.mk - 1 - ma;   // element rows above / below the anchor
+    const int HA = 4 * ma, NRW = BH + 4 * (g.mk - 1);
     uint64_t* mA = lds;
     uint64_t* mB = mA + NRW * WW;
     uint64_t* l_st = mB + NRW * WW;
@@ -1114,24 +1136,41 @@ __global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
     const uint64_t lastmask = (W & 63) ? ((1ull << (W & 63)) - 1) : ~0ull;
 
     for (int idx = tid; idx < NRW * WW; idx += nth) {
-        const int r = idx / WW, wi = idx - r * WW, y = y0 - 4 + r;
+        const int r = idx / WW, wi = idx - r * WW, y = y0 - HA + r;
         mA[idx] = (y >= 0 && y < H) ? sb[(size_t)y * WW + wi] : 0ull;
     }
     __syncthreads();
-    // passes: dilate A->B, erode B->A, erode A->B, dilate B->A
+    // passes: dilate A->B, erode B->A, erode A->B, dilate B->A; pass p has
+    // valid sources for buffer rows p*ma .. NRW-1-p*mb
 #pragma unroll
     for (int p = 1; p <= 4; ++p) {
         const uint64_t* src = (p & 1) ? mA : mB;
         uint64_t* dst = (p & 1) ? mB : mA;
         const bool dil = p == 1 || p == 4;
-        for (int idx = p * WW + tid; idx < NRW * WW; idx += nth) {
-            const int r = idx / WW, wi = idx - r * WW, y = y0 - 4 + r;
+        const int r0 = p * ma, r1 = NRW - p * mb;
+        for (int idx = r0 * WW + tid; idx < r1 * WW; idx += nth) {
+            const int r = idx / WW, wi = idx - r * WW, y = y0 - HA + r;
             if (y < 0 || y >= H) continue;
-            const uint64_t v = src[idx];
-            const uint64_t lb = wi > 0 ? (src[idx - 1] >> 63) : (dil ? 0ull : 1ull);
-            const uint64_t left = (v << 1) | lb;
-            const uint64_t up = y > 0 ? src[idx - WW] : (dil ? 0ull : ~0ull);
-            uint64_t o = dil ? (v | left | up) : (v & left & up);
+            uint64_t o;
+            if (g.mk == 2) {   // [[0,1],[1,1]]: (x, y), (x-1, y), (x, y-1)
+                const uint64_t v = src[idx];
+                const uint64_t lb = wi > 0 ? (src[idx - 1] >> 63) : (dil ? 0ull : 1ull);
+                const uint64_t left = (v << 1) | lb;
+                const uint64_t up = y > 0 ? src[idx - WW] : (dil ? 0ull : ~0ull);
+                o = dil ? (v | left | up) : (v & left & up);
+            } else {
+                const uint64_t outside = dil ? 0ull : ~0ull;
+                o = outside;
+                for (int i = 0; i < g.mk; ++i) {
+                    const int dy = i - ma, lo = g.mlo[i], hi = g.mhi[i];
+                    if (lo > hi || y + dy < 0 || y + dy >= H) continue;   // empty row / ignored pixels
+                    const uint64_t* row = src + (r + dy) * WW;
+                    for (int dx = lo; dx <= hi; ++dx) {
+                        const uint64_t v = row_bits64(row, WW, lastmask, wi * 64 + dx, outside);
+                        o = dil ? (o | v) : (o & v);
+                    }
+                }
+            }
             if (wi == WW - 1) o &= lastmask;
             dst[idx] = o;
         }
@@ -1140,7 +1179,7 @@ __global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
     // morphed rows of the band -> global
     for (int idx = tid; idx < BH * WW; idx += nth) {
         const int r = idx / WW, wi = idx - r * WW, y = y0 + r;
-        if (y < H) ob[(size_t)y * WW + wi] = mA[(r + 4) * WW + wi];
+        if (y < H) ob[(size_t)y * WW + wi] = mA[(r + HA) * WW + wi];
     }
 
     // run index + local union-find (fg, 8-connected)
@@ -1160,7 +1199,7 @@ __global__ void __launch_bounds__(512) k_of_band(OfGeom g, OfBufs B, int BH)
     uint16_t* pe = l_pe + wave * (WW + 1);
     int n = 0;
     if (act) {
-        n = build_row_idx(mA + (wave + 4) * WW, WW, W, st, en, ps, pe, nullptr);
+        n = build_row_idx(mA + (wave + HA) * WW, WW, W, st, en, ps, pe, nullptr);
         for (int i = lane; i < WW; i += 64) {
             uint64_t s = st[i], e = en[i];
             int ks = ps[i], ke = pe[i];
@@ -1327,8 +1366,12 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
     const int gb = lane >> 3, r = lane & 7;
     const int bx = (blockIdx.x * 8 + gb) * 8, by = (blockIdx.y * 4 + wave) * 8, y = by + r;
     const bool act = bx < W && y < H;
+    // px of this lane's row segment inside the frame: 8, or fewer in the
+    // partial block column at the right edge (any W, of:159,177 skip those
+    // blocks; their pixels still take the YCrCb round trip, of:170-171)
+    const int np = act ? min(8, W - bx) : 0;
     float* S = sT[wave][gb];
-    const uint64_t* rb = B.rbits + (size_t)t * H * WW;
+    const uint64_t* rb = o.mbits ? o.mbits + (size_t)t * o.mbstride : B.rbits + (size_t)t * H * WW;
     const uint32_t mrow = act ? (uint32_t)(rb[(size_t)y * WW + (bx >> 6)] >> (bx & 63)) & 0xffu : 0u;
     uint32_t any = mrow;
     any |= __shfl_xor(any, 1, 8);
@@ -1341,17 +1384,28 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
             lo |= ((mrow >> j) & 1u) ? (255u << (8 * j)) : 0u;
             hi |= ((mrow >> (j + 4)) & 1u) ? (255u << (8 * j)) : 0u;
         }
-        *reinterpret_cast<uint2*>(o.mask + (size_t)t * o.mstride + (size_t)y * W + bx) = make_uint2(lo, hi);
+        uint8_t* mp = o.mask + (size_t)t * o.mstride + (size_t)y * W + bx;
+        if (np == 8 && ((uintptr_t)mp & 7) == 0) {
+            *reinterpret_cast<uint2*>(mp) = make_uint2(lo, hi);
+        } else {   // rows of W bytes: any W
+            for (int j = 0; j < np; ++j) mp[j] = (uint8_t)((j < 4 ? lo >> (8 * j) : hi >> (8 * (j - 4))) & 255u);
+        }
     }
     if (!o.compressed) return;
     // this lane's row of the block: BGR -> YCrCb (of:156)
     int ch[3][8];
     {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(o.bgr + (size_t)t * o.fstride +
-                                                               (size_t)(act ? y : 0) * o.pitch + 3 * (act ? bx : 0));
+        const uint8_t* src8 = o.bgr + (size_t)t * o.fstride + (size_t)(act ? y : 0) * o.pitch + 3 * (act ? bx : 0);
         uint32_t px[6];
+        if (np == 8) {   // 24 bytes, dword aligned (pitch, fstride % 4 == 0; 3 bx % 24 == 0)
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(src8);
 #pragma unroll
-        for (int d = 0; d < 6; ++d) px[d] = src[d];
+            for (int d = 0; d < 6; ++d) px[d] = src[d];
+        } else {
+#pragma unroll
+            for (int d = 0; d < 6; ++d) px[d] = 0;
+            for (int k = 0; k < 3 * np; ++k) px[k >> 2] |= (uint32_t)src8[k] << (8 * (k & 3));
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int b = (px[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
@@ -1413,10 +1467,44 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
         ob[3 * j + 1] = (uint8_t)gg;
         ob[3 * j + 2] = (uint8_t)rr;
     }
-    uint32_t* d = reinterpret_cast<uint32_t*>(o.compressed + (size_t)t * o.ostride + (size_t)y * 3 * W + 3 * bx);
+    uint8_t* d8 = o.compressed + (size_t)t * o.ostride + (size_t)y * 3 * W + 3 * bx;
+    if (np == 8 && ((uintptr_t)d8 & 3) == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(d8);
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
-        d[q] = ob[4 * q] | (ob[4 * q + 1] << 8) | (ob[4 * q + 2] << 16) | ((uint32_t)ob[4 * q + 3] << 24);
+        for (int q = 0; q < 6; ++q)
+            d[q] = ob[4 * q] | (ob[4 * q + 1] << 8) | (ob[4 * q + 2] << 16) | ((uint32_t)ob[4 * q + 3] << 24);
+    } else {   // rows of 3W bytes: W % 4 != 0 leaves odd rows unaligned
+        for (int k = 0; k < 3 * np; ++k) d8[k] = ob[k];
+    }
+}
+
+// compress_with_motion's gate from a decoded mask frame (of:141-149): a
+// 3-channel mask (what VideoCapture returns for mask.mp4) is cvtColor'd to
+// gray first, exactly — a coloured pixel can gray to 0 — then "nonzero" is the
+// motion bit the block test `block_mask.mean() == 0` reads. One lane per
+// pixel, a wave per 64-px mask word (ballot), 4 words per workgroup.
+__global__ void __launch_bounds__(256) k_mask_bits(const uint8_t* __restrict__ mask, size_t mpitch, size_t mstride,
+                                                   int channels, int W, int H, int WW, uint64_t* __restrict__ bits)
+{
+    const int lane = threadIdx.x & 63, wi = blockIdx.x * 4 + (threadIdx.x >> 6), y = blockIdx.y, t = blockIdx.z;
+    if (wi >= WW) return;   // uniform per wave
+    const int x = wi * 64 + lane;
+    bool on = false;
+    if (x < W) {
+        const uint8_t* m = mask + (size_t)t * mstride + (size_t)y * mpitch;
+        on = channels == 3 ? gray_px(m[3 * x], m[3 * x + 1], m[3 * x + 2]) != 0 : m[x] != 0;
+    }
+    const unsigned long long word = __ballot(on);
+    if (lane == 0) bits[((size_t)t * H + y) * WW + wi] = word;
+}
+
+hipError_t of_launch_mask_bits(const uint8_t* mask, size_t mpitch, size_t mstride, int channels, int W, int H, int n,
+                               uint64_t* bits, hipStream_t s)
+{
+    const int WW = (W + 63) / 64;
+    hipLaunchKernelGGL(k_mask_bits, dim3((WW + 3) / 4, H, n), dim3(256), 0, s, mask, mpitch, mstride, channels, W, H,
+                       WW, bits);
+    return hipGetLastError();
 }
 
 // Static-block counter (separate tiny pass keeps k_of_out's exits simple).
@@ -1446,8 +1534,8 @@ static int of_band_rows(const OfGeom& g, size_t* lds)
 {
     int bh = 8;
     for (;;) {
-        const size_t b = (size_t)16 * (bh + 4) * g.WW + (size_t)16 * bh * g.WW + (size_t)4 * bh * (g.WW + 1) +
-                         (size_t)4 * bh * g.CAP + 16;
+        const size_t b = (size_t)16 * (bh + 4 * (g.mk - 1)) * g.WW + (size_t)16 * bh * g.WW +
+                         (size_t)4 * bh * (g.WW + 1) + (size_t)4 * bh * g.CAP + 16;
         if (b <= 150 * 1024 || bh == 1) {
             *lds = b;
             return bh;
@@ -1478,7 +1566,7 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
         else hipLaunchKernelGGL(k_of_front0<7>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
     }
     for (int k = 1; k <= g.L; ++k) {
-        hipLaunchKernelGGL(k_pyr_h, dim3(g.H, n), dim3(256), (size_t)g.W, s, g, lv[k], b.gray);
+        hipLaunchKernelGGL(k_pyr_h, dim3(g.H, n), dim3(256), (size_t)g.GP, s, g, lv[k], b.gray);
         hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, 2 * lv[k].h, n), dim3(256), 0, s, g, lv[k]);
         dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);
         if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, s, g, lv[k], a0);
@@ -1518,8 +1606,9 @@ __global__ void __launch_bounds__(256) k_flow_up(FlowArgs A, float* __restrict__
     if (x0 + 4 <= w && !(w & 1)) {   // 16-B aligned: x0 % 4 == 0 and rows of an even width
         *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-        for (int k = 0; k < w - x0; ++k) *reinterpret_cast<float2*>(o + 2 * k) = make_float2(v[2 * k], v[2 * k + 1]);
+    } else {   // the row's last lane, or rows of an odd width (8-B aligned only)
+        const int np = min(4, w - x0);
+        for (int k = 0; k < np; ++k) *reinterpret_cast<float2*>(o + 2 * k) = make_float2(v[2 * k], v[2 * k + 1]);
     }
 }
 
@@ -1633,7 +1722,8 @@ hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int wi
 hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s)
 {
     if (!o.mask && !o.compressed) return hipSuccess;
-    dim3 grid((g.W / 8 + 7) / 8, (g.H / 8 + 3) / 4, n);
+    const int nbx = (g.W + 7) / 8, nby = (g.H + 7) / 8;   // partial edge blocks included (pixels, not DCT)
+    dim3 grid((nbx + 7) / 8, (nby + 3) / 4, n);
     hipLaunchKernelGGL(k_of_out, grid, dim3(256), 0, s, g, b, o);
     return hipGetLastError();
 }

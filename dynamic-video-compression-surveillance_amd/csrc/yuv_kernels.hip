@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "../../include/dvc.h"
 #include "host_common.h"
@@ -151,6 +153,60 @@ int check_yuv_args(int fmt, int crows, int W, int H, size_t pitch, int n, size_t
     return DVC_OK;
 }
 
+// Device scratch of the host-pointer conversions (a Y4M reader / writer thread
+// calls them once per frame): kept across calls instead of hipMalloc/hipFree
+// per call — hipFree synchronises the whole device, which would stall every
+// worker's pipelined streams. A call takes an entry of its device (or makes
+// one), grows it when a frame is larger, and gives it back; entries live until
+// the process ends. Each entry has its own non-blocking stream for callers
+// that pass none (the legacy default stream would serialise with the rest).
+struct Scratch {
+    int device = 0;
+    uint8_t *a = nullptr, *b = nullptr;
+    size_t na = 0, nb = 0;
+    hipStream_t stream = nullptr;
+};
+
+std::mutex g_scratch_mu;
+std::vector<Scratch*> g_scratch_free;
+
+Scratch* scratch_take(int device)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        for (size_t i = 0; i < g_scratch_free.size(); ++i)
+            if (g_scratch_free[i]->device == device) {
+                Scratch* s = g_scratch_free[i];
+                g_scratch_free.erase(g_scratch_free.begin() + (long)i);
+                return s;
+            }
+    }
+    Scratch* s = new Scratch();
+    s->device = device;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+void scratch_give(Scratch* s)
+{
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    g_scratch_free.push_back(s);
+}
+
+hipError_t scratch_fit(uint8_t** p, size_t* have, size_t need)
+{
+    if (*have >= need) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    hipError_t e = hipMalloc(p, need);
+    if (e == hipSuccess) *have = need;
+    return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -173,11 +229,14 @@ int dvc_yuv420_to_bgr(const uint8_t* yuv, size_t pitch, int fmt, int chroma_rows
                                          bgr_pitch, bgr_stride, st));
         return DVC_OK;
     }
-    // host pointers: one frame at a time through device buffers, synchronous
+    // host pointers: one frame at a time through the device scratch, synchronous
     const size_t fb = dvc::yuv_frame_bytes(pitch, cr), ob = 3 * (size_t)width * height;
-    uint8_t *din = nullptr, *dout = nullptr;
-    HIP_OK(hipMalloc(&din, fb));
-    hipError_t e = hipMalloc(&dout, ob);
+    Scratch* sc = scratch_take(device);
+    if (!sc) return fail(DVC_E_HIP, "yuv420 -> bgr: no stream");
+    if (!st) st = sc->stream;
+    hipError_t e = scratch_fit(&sc->a, &sc->na, fb);
+    if (e == hipSuccess) e = scratch_fit(&sc->b, &sc->nb, ob);
+    uint8_t *din = sc->a, *dout = sc->b;
     for (int t = 0; t < n && e == hipSuccess; ++t) {
         e = hipMemcpyAsync(din, yuv + (size_t)t * frame_stride, fb, hipMemcpyHostToDevice, st);
         if (e == hipSuccess)
@@ -188,8 +247,7 @@ int dvc_yuv420_to_bgr(const uint8_t* yuv, size_t pitch, int fmt, int chroma_rows
                                  height, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
     }
-    (void)hipFree(din);
-    if (dout) (void)hipFree(dout);
+    scratch_give(sc);
     if (e != hipSuccess) return fail(DVC_E_HIP, "yuv420 -> bgr: %s", hipGetErrorString(e));
     return DVC_OK;
 }
@@ -213,9 +271,12 @@ int dvc_bgr_to_i420(const uint8_t* bgr, size_t bgr_pitch, size_t bgr_stride, int
         return DVC_OK;
     }
     const size_t fb = dvc::yuv_frame_bytes(pitch, cr), ib = 3 * (size_t)width * height;
-    uint8_t *din = nullptr, *dout = nullptr;
-    HIP_OK(hipMalloc(&din, ib));
-    hipError_t e = hipMalloc(&dout, fb);
+    Scratch* sc = scratch_take(device);
+    if (!sc) return fail(DVC_E_HIP, "bgr -> i420: no stream");
+    if (!st) st = sc->stream;
+    hipError_t e = scratch_fit(&sc->a, &sc->na, ib);
+    if (e == hipSuccess) e = scratch_fit(&sc->b, &sc->nb, fb);
+    uint8_t *din = sc->a, *dout = sc->b;
     for (int t = 0; t < n && e == hipSuccess; ++t) {
         e = hipMemcpy2DAsync(din, 3 * (size_t)width, bgr + (size_t)t * bgr_stride, bgr_pitch, 3 * (size_t)width,
                              height, hipMemcpyHostToDevice, st);
@@ -226,8 +287,7 @@ int dvc_bgr_to_i420(const uint8_t* bgr, size_t bgr_pitch, size_t bgr_stride, int
         if (e == hipSuccess) e = hipMemcpyAsync(yuv + (size_t)t * frame_stride, dout, fb, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
     }
-    (void)hipFree(din);
-    if (dout) (void)hipFree(dout);
+    scratch_give(sc);
     if (e != hipSuccess) return fail(DVC_E_HIP, "bgr -> i420: %s", hipGetErrorString(e));
     return DVC_OK;
 }

@@ -151,7 +151,6 @@ def filter_and_dilate_movements(video_path, output_dir,
                 break
             j = pipe.out_buffer()
             ov, cp = pipe.outs[j]
-            t0 = time.time()
             stop = None
             try:                                                # fd:91-133, n times
                 worker.step_batch(pipe.ins[i][:n], ov[:n], cp[:n])
@@ -160,7 +159,6 @@ def filter_and_dilate_movements(video_path, output_dir,
                 if e.code != DVC_E_ODD_DCT:
                     raise
                 stop, done = e, worker.stats()["frames"] - handed
-            per_frame_s.extend([(time.time() - t0) / n] * done)
             pipe.write(i, j, done, stop is not None)
             handed += done
             if stop is not None:
@@ -175,6 +173,8 @@ def filter_and_dilate_movements(video_path, output_dir,
     finally:
         if reader is not None:
             pipe.stop()
+            # fd:86,135 per frame: read -> last write, as the run sees it (_dropin.py)
+            per_frame_s = pipe.frame_times()[:sinks.frames]
         cap.release()
         sinks.release()
         if worker is not None:

@@ -18,16 +18,16 @@ functions return ``(0, 0, 0)`` / ``None`` as the reference does
 (``of:40-42, 55-58, 123-128``).
 
 The per-frame work runs on the GPU: ``OFWorker`` (Farneback, vote, close/open,
-rectangles; of:70-97) and ``dvc_of_compress`` (of:151-183) — never a CPU
-fallback.
+rectangles; of:70-97) and ``OFCompressor`` / ``dvc_ofc_run`` (of:141-185) —
+never a CPU fallback. Both loops run in chunks through ``ChunkPipeline``
+(reader / GPU / writer threads). ``avg_s`` is total / frames, as of:106,190
+compute it.
 """
 from __future__ import annotations
 
 import logging
 import os
 import time
-
-import numpy as np
 
 from . import _native as N
 from ._dropin import ChunkPipeline
@@ -60,12 +60,6 @@ def setup_logging(output_dir):
 
 def _device() -> int:
     return int(os.environ.get("DVC_DEVICE", os.environ.get("LOCAL_RANK", 0)))
-
-
-def _bgr2gray(frame: np.ndarray) -> np.ndarray:
-    """cv2.cvtColor(BGR2GRAY) for 8U: (1868 B + 9617 G + 4899 R + 2^13) >> 14."""
-    f = frame.astype(np.uint32)
-    return ((f[..., 0] * 1868 + f[..., 1] * 9617 + f[..., 2] * 4899 + 8192) >> 14).astype(np.uint8)
 
 
 def temporal_smoothing_flow(video_path, output_dir, flow_threshold=0.5, alpha_fraction=0.2,
@@ -137,7 +131,13 @@ def temporal_smoothing_flow(video_path, output_dir, flow_threshold=0.5, alpha_fr
 
 
 def compress_with_motion(input_video, mask_video, output_dir, quantization_level=100):
-    """of:111-193: static 8x8 blocks (mask all zero) DCT-quantised on Y, Cr, Cb, then grey."""
+    """of:111-193: static 8x8 blocks (mask all zero) DCT-quantised on Y, Cr, Cb, then grey.
+
+    The loop of:141-185 runs READ_AHEAD frame pairs per ``dvc_ofc_run`` call
+    (``_native.OFCompressor``; identical to one call per frame): a reader thread
+    reads the input and mask videos in lockstep into page-locked chunks (of:142-
+    143, stopping at the shorter one), the GPU grays 3-channel masks (of:147-149)
+    and compresses the chunk, a writer thread writes ``compressed.mp4`` (of:185)."""
     start_time = time.time()
     logging.info(f"Starting motion-based compression for: {os.path.basename(input_video)}")
     cap_input = video_io.open_source(input_video)
@@ -153,19 +153,49 @@ def compress_with_motion(input_video, mask_video, output_dir, quantization_level
     height = int(cap_input.get(video_io.CAP_PROP_FRAME_HEIGHT))
     out = video_io.open_sink(os.path.join(output_dir, "compressed.mp4"), fps, (width, height))
     frame_count = 0
+    comp = pipe = None
     try:
-        while True:
-            ret_in, frame_in = cap_input.read()
-            ret_mask, frame_mask = cap_mask.read()
-            if not (ret_in and ret_mask):
-                break
-            frame_count += 1
-            if len(frame_mask.shape) == 3:
-                frame_mask = _bgr2gray(frame_mask)
-            out.write(N.of_compress(frame_in, frame_mask, float(quantization_level), device=_device()))
+        ret_in, frame_in = cap_input.read()
+        ret_mask, frame_mask = cap_mask.read()
+        if ret_in and ret_mask:
+            first = [(frame_in, frame_mask)]
+
+            def read_pair():   # of:142-145: both videos, stop at the first missing frame
+                if first:
+                    return True, first.pop()
+                ok_a, a = cap_input.read()
+                ok_b, b = cap_mask.read()
+                return (ok_a and ok_b), (a, b)
+
+            R = max(1, READ_AHEAD)
+            mshape = tuple(frame_mask.shape)   # (H, W) or (H, W, 3) as decoded
+            comp = N.OFCompressor(width, height, float(quantization_level), max_batch=R, device=_device())
+
+            def emit(i, outs, done, failing):
+                for t in range(done):
+                    out.write(outs[0][t])
+
+            pipe = ChunkPipeline(R, [(height, width, 3), mshape], [(height, width, 3)], read_pair, emit)
+            pipe.start()
+            while True:
+                i, n = pipe.next_chunk()
+                if n == 0:
+                    break
+                j = pipe.out_buffer()
+                frames, masks = pipe.ins[i]
+                comp.run(frames[:n], masks[:n], out=pipe.outs[j][0][:n])
+                pipe.write(i, j, n)
+                frame_count += n
+                if n < R:
+                    break
+            pipe.finish()
     except Exception as e:
         logging.error(f"Error during compression: {e}", exc_info=True)
     finally:
+        if pipe is not None:
+            pipe.stop()
+        if comp is not None:
+            comp.close()
         cap_input.release()
         cap_mask.release()
         out.release()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 5
+#define DVC_ABI_VERSION 6
 #define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
@@ -380,14 +380,45 @@ int dvc_of_debug_read(dvc_of* h, int what, int level, void* host_dst, int* w, in
 
 /* compress_with_motion for one frame with an arbitrary mask (of:141-185, e.g.
  * a decoded mask.mp4 frame): host pointers, synchronous. mask: H*W bytes,
- * nonzero = motion. W, H multiples of 8. */
+ * nonzero = motion. Any W, H >= 1: partial 8x8 edge blocks are never
+ * compressed (of:159,177) but take the YCrCb round trip (of:170-171). */
 int dvc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int width, int height, float quant,
                     int device, uint8_t* out);
+
+/* compress_with_motion (motion_compression_opt.py:111-193) as a handle, n
+ * frames per call: replaces the loop of:141-185 — its two reads (of:142-143),
+ * the 3-channel mask's BGR2GRAY (of:147-149, exact: a coloured pixel can gray
+ * to 0), the static full 8x8 blocks' DCT quantisation of Y, Cr, Cb, YCrCb->BGR
+ * and per-block gray (of:151-183) — for frames t = 0..n-1:
+ *   bgr + t*frame_stride      BGR rows of `pitch` (>= 3W)
+ *   mask + t*mask_stride      mask rows of `mask_pitch`, mask_channels 1 (gray)
+ *                             or 3 (BGR, as VideoCapture decodes mask.mp4)
+ *   out + t*out_stride        compressed BGR rows of 3W (of:185)
+ * Results identical to n dvc_of_compress calls (with the masks grayed).
+ * quant = QTY_aggressive's constant (of:138, 100). Host pointers: synchronous
+ * per call; DVC_FLAG_DEVICE_PTRS: device pointers, asynchronous on hip_stream
+ * (NULL: the handle's own stream; dvc_ofc_sync waits). */
+typedef struct dvc_ofc dvc_ofc;
+int dvc_ofc_create(int width, int height, float quant, int max_batch, int device, void* hip_stream, uint32_t flags,
+                   dvc_ofc** out);
+int dvc_ofc_run(dvc_ofc* h, const uint8_t* bgr, size_t pitch, size_t frame_stride, const uint8_t* mask,
+                size_t mask_pitch, size_t mask_stride, int mask_channels, int n, uint8_t* out, size_t out_stride);
+int dvc_ofc_sync(dvc_ofc* h);
+void dvc_ofc_destroy(dvc_ofc* h);
 
 /* The Q8 fixed-point Gaussian taps OpenCV's bit-exact 8U GaussianBlur uses
  * (getGaussianKernelBitExact + error-diffusion rounding to 8 fraction bits).
  * n odd, 1 <= n <= 63. Exposed for the parity tests. */
 int dvc_gaussian_taps_q8(int n, double sigma, uint16_t* taps);
+
+/* ---- diagnostics ----------------------------------------------------------- */
+/* Not a reference interface: the measurement bench.py quotes the FD roofline
+ * against beside the 8 TB/s spec (SURVEY.md §8d "fraction of measured
+ * stream-copy bandwidth on the same box"). A hand-written 16-B-per-lane copy
+ * of `bytes` (use >> 256 MB, the Infinity Cache) repeated `reps` times on
+ * `device`, nontemporal stores if `nontemporal`; *gbps = bytes read + written
+ * per second / 1e9. */
+int dvc_copy_rate(int device, size_t bytes, int reps, int nontemporal, double* gbps);
 
 #ifdef __cplusplus
 }

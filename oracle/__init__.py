@@ -454,6 +454,8 @@ def _of_lib():
         L.oc_farneback.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, fp]
         L.oc_morph_close_open.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_morph_close_open_k.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p]
+        L.oc_ellipse_element.argtypes = [ctypes.c_int, u8p]
         L.oc_rect_mask.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
         L.oc_rect_mask.restype = ctypes.c_int64
         L.oc_of_compress.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_int, ctypes.c_int, ctypes.c_float, u8p]
@@ -510,11 +512,19 @@ def fb_iteration(R0: np.ndarray, R1: np.ndarray, flow: np.ndarray, winsize=9, sl
     return f
 
 
-def morph_close_open(m: np.ndarray) -> np.ndarray:
+def morph_close_open(m: np.ndarray, k: int = 2) -> np.ndarray:
+    """of:89-90 with getStructuringElement(MORPH_ELLIPSE, (k, k)) (of:62)."""
     m = np.ascontiguousarray(m, np.uint8)
     out = np.empty_like(m)
-    _of_lib().oc_morph_close_open(_u8(m), m.shape[1], m.shape[0], _u8(out))
+    _of_lib().oc_morph_close_open_k(_u8(m), m.shape[1], m.shape[0], int(k), _u8(out))
     return out
+
+
+def ellipse_element(k: int) -> np.ndarray:
+    """getStructuringElement(MORPH_ELLIPSE, (k, k)) as the oracle restates it (k x k, 0/1)."""
+    el = np.empty((k, k), np.uint8)
+    _of_lib().oc_ellipse_element(int(k), _u8(el))
+    return el
 
 
 def rect_mask(m: np.ndarray):

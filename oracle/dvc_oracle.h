@@ -57,6 +57,8 @@ void oc_fb_level_poly(const uint8_t* gray, int W, int H, double pyr_scale, int k
 void oc_farneback(const uint8_t* prev, const uint8_t* next, int W, int H, double pyr_scale, int levels,
                   int winsize, int iterations, int poly_n, double poly_sigma, float* flow_out);
 void oc_morph_close_open(const uint8_t* src, int W, int H, uint8_t* dst);
+void oc_morph_close_open_k(const uint8_t* src, int W, int H, int k, uint8_t* dst);
+void oc_ellipse_element(int k, uint8_t* el);
 int64_t oc_rect_mask(const uint8_t* m, int W, int H, uint8_t* out);
 void oc_of_compress(const uint8_t* bgr, size_t pitch, const uint8_t* mask, int W, int H, float q, uint8_t* out);
 int oc_vote_threshold(double alpha, int L);

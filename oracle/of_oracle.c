@@ -9,7 +9,8 @@
  *   gray (of:60,71) -> calcOpticalFlowFarneback(prev, gray, 0.3, 2, 9, 2, 5, 1.1, 0)
  *   (of:72-81) -> |flow| > 0.5 (of:82-83) -> vote over the last `window` masks,
  *   count*255 >= alpha*L*255 (of:84-86) -> MORPH_CLOSE then MORPH_OPEN with the
- *   2x2 ellipse [[0,1],[1,1]] (of:89-90) -> union of the external contours'
+ *   morph_kernel x morph_kernel ellipse (of:62,89-90; default 2 = [[0,1],[1,1]])
+ *   -> union of the external contours'
  *   bounding rectangles grown by one pixel right/down (of:93-97) -> on every full
  *   8x8 block whose mask is all zero: DCT quantisation of Y, Cr and Cb
  *   (of:156-168), YCrCb->BGR (of:170-171), then BGR->gray->BGR (of:174-183).
@@ -430,29 +431,66 @@ void oc_farneback(const uint8_t* prev, const uint8_t* next, int W, int H, double
     free(prev_flow);
 }
 
-/* morphologyEx with the 2x2 ellipse [[0,1],[1,1]], anchor (1,1): window
- * offsets (0,0), (-1,0), (0,-1); out-of-image pixels are ignored. */
-static void morph2(const uint8_t* s, int W, int H, int dilate, uint8_t* d)
+/* getStructuringElement(MORPH_ELLIPSE, (k, k)) (of:62; OpenCV 4.11
+ * imgproc/morph.dispatch.cpp): r = c = k/2, inv_r2 = r ? 1/(r*r) : 0; row i
+ * has dy = i - r and, when |dy| <= r, ones at columns [max(c - dx, 0),
+ * min(c + dx + 1, k)) with dx = saturate_cast<int>(c * sqrt((r*r - dy*dy) *
+ * inv_r2)) (cvRound: half to even); k = 1 is MORPH_RECT, the same [[1]].
+ * k = 2 gives [[0,1],[1,1]]. el: k*k bytes. */
+void oc_ellipse_element(int k, uint8_t* el)
 {
+    const int r = k / 2, c = k / 2;
+    const double inv_r2 = r ? 1. / ((double)r * r) : 0;
+    memset(el, 0, (size_t)k * k);
+    for (int i = 0; i < k; ++i) {
+        const int dy = i - r;
+        if (abs(dy) > r) continue;
+        const int dx = (int)lrint(c * sqrt((r * r - dy * dy) * inv_r2));
+        const int j1 = c - dx > 0 ? c - dx : 0, j2 = c + dx + 1 < k ? c + dx + 1 : k;
+        for (int j = j1; j < j2; ++j) el[i * k + j] = 1;
+    }
+}
+
+/* dilate / erode with a k x k element, anchor (k/2, k/2) (the default (-1,-1)):
+ * out(x, y) = max / min over el[i][j] != 0 of src(x + j - k/2, y + i - k/2);
+ * out-of-image pixels are ignored (morphologyDefaultBorderValue). */
+static void morph_el(const uint8_t* s, int W, int H, const uint8_t* el, int k, int dilate, uint8_t* d)
+{
+    const int a = k / 2;
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
-            uint8_t v = s[(size_t)y * W + x];
-            if (x > 0) { uint8_t u = s[(size_t)y * W + x - 1]; v = dilate ? (u > v ? u : v) : (u < v ? u : v); }
-            if (y > 0) { uint8_t u = s[(size_t)(y - 1) * W + x]; v = dilate ? (u > v ? u : v) : (u < v ? u : v); }
-            d[(size_t)y * W + x] = v;
+            int v = dilate ? 0 : 255;
+            for (int i = 0; i < k; ++i) {
+                const int yy = y + i - a;
+                if (yy < 0 || yy >= H) continue;
+                for (int j = 0; j < k; ++j) {
+                    const int xx = x + j - a;
+                    if (!el[i * k + j] || xx < 0 || xx >= W) continue;
+                    const int u = s[(size_t)yy * W + xx];
+                    v = dilate ? (u > v ? u : v) : (u < v ? u : v);
+                }
+            }
+            d[(size_t)y * W + x] = (uint8_t)v;
         }
 }
 
-void oc_morph_close_open(const uint8_t* src, int W, int H, uint8_t* dst)
+/* of:89-90: morphologyEx(MORPH_CLOSE) then morphologyEx(MORPH_OPEN) with
+ * getStructuringElement(MORPH_ELLIPSE, (k, k)): dilate, erode, erode, dilate. */
+void oc_morph_close_open_k(const uint8_t* src, int W, int H, int k, uint8_t* dst)
 {
+    uint8_t* el = (uint8_t*)malloc((size_t)k * k);
     uint8_t* a = (uint8_t*)malloc((size_t)W * H);
     uint8_t* b = (uint8_t*)malloc((size_t)W * H);
-    morph2(src, W, H, 1, a);   /* close = dilate, erode */
-    morph2(a, W, H, 0, b);
-    morph2(b, W, H, 0, a);     /* open = erode, dilate */
-    morph2(a, W, H, 1, dst);
-    free(a); free(b);
+    oc_ellipse_element(k, el);
+    morph_el(src, W, H, el, k, 1, a);   /* close = dilate, erode */
+    morph_el(a, W, H, el, k, 0, b);
+    morph_el(b, W, H, el, k, 0, a);     /* open = erode, dilate */
+    morph_el(a, W, H, el, k, 1, dst);
+    free(el); free(a); free(b);
 }
+
+/* the reference's default element, [[0,1],[1,1]] (k = 2, of:62) */
+void oc_morph_close_open(const uint8_t* src, int W, int H, uint8_t* dst) { oc_morph_close_open_k(src, W, H, 2, dst); }
 
 /* of:93-97: union of (bounding rectangle grown by one px right/down) of every
  * 8-connected component (nested ones lie inside their parent's rectangle, so
@@ -549,7 +587,7 @@ struct oc_of {
 
 oc_of* oc_of_create(const dvc_of_params* p)
 {
-    if (p->width < 1 || p->height < 1 || p->window < 1) return NULL;
+    if (p->width < 1 || p->height < 1 || p->window < 1 || p->morph_kernel < 1) return NULL;
     oc_of* h = (oc_of*)calloc(1, sizeof(oc_of));
     h->p = *p;
     size_t N = (size_t)p->width * p->height;
@@ -616,7 +654,7 @@ int oc_of_step(oc_of* h, const uint8_t* bgr, size_t pitch, uint8_t* mask, uint8_
     if (h->L < p->window) h->L++;
     int thr = oc_vote_threshold(p->alpha_fraction, h->L);                          /* of:85-86 */
     for (size_t i = 0; i < N; ++i) h->smooth[i] = h->cnt[i] >= thr ? 255 : 0;
-    oc_morph_close_open(h->smooth, W, H, h->morph);                                 /* of:89-90 */
+    oc_morph_close_open_k(h->smooth, W, H, p->morph_kernel, h->morph);             /* of:89-90 */
     oc_rect_mask(h->morph, W, H, h->rect);                                          /* of:93-97 */
     if (mask) memcpy(mask, h->rect, N);
     if (compressed) oc_of_compress(bgr, pitch, h->rect, W, H, p->quant, compressed); /* of:141-183 */

@@ -1,7 +1,9 @@
 """Golden cases of the OF path shared by make_golden_of.py (capture) and the
 parity tests (replay). Inputs are regenerated from these factories; the fixture
-of_golden.json keeps their SHA-256 so generator drift is caught. Sizes are
-multiples of 8 (the GPU path's constraint) and cover pyramid depths 0, 1 and 2."""
+of_golden.json keeps their SHA-256 so generator drift is caught. Sizes cover
+pyramid depths 0, 1 and 2, sides that are not multiples of 8 (partial 8x8
+edge blocks, skipped by compress_with_motion, of:159,177; rows that are not
+whole dword quads) and morph_kernel values other than the default 2 (of:62)."""
 import numpy as np
 
 from dvc_amd.synthetic import clip
@@ -15,6 +17,11 @@ CASES = {
     "of_s320_alpha0": (lambda: clip(320, 176, 4, seed=3, n_objects=2), {"alpha_fraction": 0.0}),
     "of_s640_seed0": (lambda: clip(640, 360, 5, seed=0), {}),                                # 3 levels
     "of_s640_noisy_thr03": (lambda: clip(640, 360, 5, seed=6, noisy=True), {"flow_threshold": 0.3}),
+    "of_s162x98": (lambda: clip(162, 98, 6, seed=12, n_objects=3), {}),                      # partial blocks
+    "of_s170x100_morph3": (lambda: clip(170, 100, 6, seed=13, n_objects=3), {"morph_kernel": 3}),
+    "of_s133x75_morph5_w3": (lambda: clip(133, 75, 7, seed=14, n_objects=3),                  # odd sides
+                             {"morph_kernel": 5, "window_size": 3, "alpha_fraction": 0.4}),
+    "of_s330x186_morph4": (lambda: clip(330, 186, 5, seed=15, n_objects=4), {"morph_kernel": 4}),   # 2 levels
 }
 # cases whose every output pixel is stored in of_golden.npz (the rest: SHA-256 per frame)
-FULL_ARRAYS = ("of_s160_clean", "of_noise64")
+FULL_ARRAYS = ("of_s160_clean", "of_noise64", "of_s162x98", "of_s170x100_morph3")

@@ -89,3 +89,70 @@ def test_writer_error_surfaces():
             pipe.write(i, pipe.out_buffer(), n)
         pipe.finish()
     pipe.stop()
+
+
+def test_frame_times_sum_to_loop_time():
+    """execution_times.txt's per-frame time (fd:86,135): one entry per written
+    frame, positive, and frames x average <= the wall time around the loop —
+    the reference's sequential loop gives exactly that sum."""
+    import time
+
+    frames, read = _source(23)
+    slow_read = lambda: (time.sleep(0.002), read())[1]   # noqa: E731
+    pipe = ChunkPipeline(4, (2, 3), [(2, 3)], slow_read, lambda i, outs, done, failing: time.sleep(0.003),
+                         alloc=lambda s: np.zeros(s, np.uint8))
+    t0 = time.time()
+    pipe.start()
+    try:
+        while True:
+            i, n = pipe.next_chunk()
+            if n == 0:
+                break
+            j = pipe.out_buffer()
+            time.sleep(0.004)                               # the "step"
+            pipe.write(i, j, n)
+            if n < 4:
+                break
+        pipe.finish()
+    finally:
+        pipe.stop()
+    total = time.time() - t0
+    ft = pipe.frame_times()
+    assert len(ft) == 23 and all(t > 0 for t in ft)
+    assert sum(ft) <= total + 1e-6
+    assert sum(ft) >= 0.5 * total                           # the loop is the run
+
+
+
+def test_two_videos_in_lockstep():
+    """compress_with_motion reads the input and mask videos together (of:142-
+    145) and stops at the shorter one: a list of input shapes gives one chunk
+    array per video."""
+    a = iter([np.full((2, 3), t, np.uint8) for t in range(9)])
+    b = iter([np.full((2,), 100 + t, np.uint8) for t in range(7)])
+
+    def read():
+        x, y = next(a, None), next(b, None)
+        return (x is not None and y is not None), (x, y)
+    got = []
+    pipe = ChunkPipeline(3, [(2, 3), (2,)], [(2,)], read,
+                         lambda i, outs, done, failing: got.extend(outs[0][t].copy() for t in range(done)),
+                         alloc=lambda s: np.zeros(s, np.uint8))
+    pipe.start()
+    try:
+        while True:
+            i, n = pipe.next_chunk()
+            if n == 0:
+                break
+            fa, fb = pipe.ins[i]
+            j = pipe.out_buffer()
+            pipe.outs[j][0][:n] = fa[:n, :, 0] + fb[:n]
+            pipe.write(i, j, n)
+            if n < 3:
+                break
+        pipe.finish()
+    finally:
+        pipe.stop()
+    assert len(got) == 7
+    for t, g in enumerate(got):
+        assert np.array_equal(g, np.full((2,), 100 + 2 * t, np.uint8))

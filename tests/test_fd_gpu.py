@@ -266,6 +266,11 @@ def test_process_single_video_fd(gpu_lib, tmp_path):
     txt = (d / "execution_times.txt").read_text().splitlines()
     assert txt[0] == "Frame Differencing:" and txt[1] == "  Frames processed: 101"
     assert (d / "processing.log").exists()
+    # per-frame time as fd:86,135 sums it: read -> write of every frame adds up
+    # to the loop, so frames x average <= total (rounding of the 2/4 decimals)
+    total = float(txt[2].split(":")[1].split()[0])
+    avg = float(txt[3].split(":")[1].split()[0])
+    assert 0 < avg and 101 * avg <= total + 101 * 5e-5 + 5e-3
 
 
 def test_process_single_video_fd_chunks_and_odd_dct_stop(gpu_lib, tmp_path, monkeypatch, caplog):

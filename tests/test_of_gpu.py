@@ -36,7 +36,8 @@ def _run_pair(dvc_amd, oracle, frames, batch=0, **kw):
         raw = ref.plane(0)
         motion += int((raw > 0).sum())
         comps += oracle.rect_mask(ref.plane(2))[1]
-        static += int((rmask.reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3)) == 0).sum())
+        full = rmask[:H // 8 * 8, :W // 8 * 8]        # partial edge blocks are never static (of:159)
+        static += int((full.reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3)) == 0).sum())
         if batch:
             continue
         mask, cp = gpu.step(frames[t])
@@ -63,7 +64,7 @@ def _run_pair(dvc_amd, oracle, frames, batch=0, **kw):
     return st
 
 
-@pytest.mark.parametrize("W,H", [(160, 96), (640, 360)])
+@pytest.mark.parametrize("W,H", [(160, 96), (640, 360), (333, 185), (170, 100)])
 def test_of_stages(gpu_lib, oracle_lib, W, H):
     """Stage by stage on one frame pair: gray, the polynomial expansion of every
     pyramid level, the coarsest level's first iteration, the final flow."""
@@ -186,9 +187,10 @@ def test_of_compress_arbitrary_mask(gpu_lib, oracle_lib, density):
 
 def test_of_rejects_unsupported(gpu_lib):
     with pytest.raises(gpu_lib._native.DvcError):
-        gpu_lib.OFWorker(642, 360)          # not a multiple of 8
-    with pytest.raises(gpu_lib._native.DvcError):
-        gpu_lib.OFWorker(640, 360, morph_kernel=3)
+        gpu_lib.OFWorker(7, 360)            # frames of at least 8 x 8
+    for k in (0, 32):                       # morph_kernel 1..31
+        with pytest.raises(gpu_lib._native.DvcError):
+            gpu_lib.OFWorker(640, 360, morph_kernel=k)
     w = gpu_lib.OFWorker(160, 96)
     with pytest.raises(gpu_lib._native.DvcError):
         w.step(np.zeros((96, 160, 3), np.uint8))   # step before prime
@@ -217,3 +219,122 @@ def test_process_single_video_of_dropin(gpu_lib, oracle_lib, tmp_path):
         assert np.array_equal(cp.read()[1], rcp), t
     txt = open(out / "execution_times.txt").read()
     assert txt.startswith("Motion Detection:\n  Frames processed: 6\n") and "Compression:\n  Frames processed: 6\n" in txt
+
+
+# ---------------------------------------------------------------- geometry ---
+# The reference runs at any frame size (Farneback, the vote and the morphology
+# are per pixel; compress_with_motion skips partial 8x8 blocks, of:159,177) and
+# takes morph_kernel as a kwarg (of:29-31,62: getStructuringElement(MORPH_ELLIPSE)).
+@pytest.mark.parametrize("W,H,n,kw", [
+    (162, 98, 5, {}),                                   # W % 8 = 2, H % 8 = 2: partial blocks, 2-px quads
+    (170, 100, 5, dict(morph_kernel=3)),
+    (133, 75, 6, dict(morph_kernel=5, window_size=3, batch=2)),   # odd sides, batched
+    (333, 185, 4, dict(morph_kernel=4)),                # even element: asymmetric anchor, 2 levels
+    (97, 61, 5, dict(morph_kernel=1)),                  # 1x1 element (MORPH_RECT): identity
+    (203, 117, 4, dict(morph_kernel=9, flow_threshold=0.3)),
+])
+def test_of_any_geometry(gpu_lib, oracle_lib, W, H, n, kw):
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=W + H, n_objects=3), **kw)
+
+
+def test_of_1366x768(gpu_lib, oracle_lib):
+    """A common camera size that is not a multiple of 8 (1366 = 170 * 8 + 6)."""
+    from dvc_amd.synthetic import clip
+    _run_pair(gpu_lib, oracle_lib, clip(1366, 768, 3, seed=5))
+
+
+@pytest.mark.parametrize("k", [3, 7])
+def test_of_morph_kernel_planes(gpu_lib, oracle_lib, k):
+    """The close/open plane itself (of:89-90) against the oracle's restatement of
+    getStructuringElement + morphologyEx, on vote planes dense enough to matter."""
+    rng = np.random.default_rng(k)
+    frames = rng.integers(0, 256, (5, 72, 136, 3), dtype=np.uint8)
+    _run_pair(gpu_lib, oracle_lib, frames, morph_kernel=k, flow_threshold=1.0, window_size=2)
+
+
+@pytest.mark.parametrize("W,H,pad", [(170, 100, 0), (162, 98, 6), (320, 176, 4)])
+def test_of_device_pointers_any_pitch(gpu_lib, oracle_lib, W, H, pad):
+    """Device frames whose rows the kernels cannot read in place (3W % 4 != 0, or
+    rows padded to a pitch that is not whole quads) are re-pitched on the GPU."""
+    import torch
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, 5, seed=W, n_objects=3)
+    n = len(frames)
+    pitch = 3 * W + pad
+    buf = np.zeros((n, H, pitch), np.uint8)
+    buf[:, :, :3 * W] = frames.reshape(n, H, 3 * W)
+    d_in = torch.from_numpy(buf).to("cuda:0")
+    d_mask = torch.empty((n - 1, H, W), dtype=torch.uint8, device="cuda:0")
+    d_cp = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda:0")
+    w = gpu_lib.OFWorker(W, H, device_ptrs=True, max_batch=2)
+    lib = gpu_lib._native.lib()
+    gpu_lib._native.check(lib.dvc_of_prime(w._h, d_in[0].data_ptr(), pitch))
+    gpu_lib._native.check(lib.dvc_of_step_batch(w._h, d_in[1].data_ptr(), pitch, H * pitch, n - 1,
+                                                 d_mask.data_ptr(), H * W, d_cp.data_ptr(), 3 * H * W))
+    w.sync()
+    ref = oracle_lib.OracleOF(W, H)
+    ref.prime(frames[0])
+    for t in range(1, n):
+        rmask, rcp, _ = ref.step(frames[t])
+        assert np.array_equal(d_mask[t - 1].cpu().numpy(), rmask), t
+        assert np.array_equal(d_cp[t - 1].cpu().numpy(), rcp), t
+    w.close()
+
+
+# ------------------------------------------------------------- compressor ----
+def _gray(m3):
+    m = m3.astype(np.uint32)
+    return ((m[..., 0] * 1868 + m[..., 1] * 9617 + m[..., 2] * 4899 + 8192) >> 14).astype(np.uint8)
+
+
+@pytest.mark.parametrize("W,H,ch", [(200, 120, 1), (203, 117, 3), (64, 64, 3), (1366, 10, 1)])
+def test_ofc_batch_equals_per_frame(gpu_lib, oracle_lib, W, H, ch):
+    """dvc_ofc (compress_with_motion's loop, of:141-185, n frames per call) ==
+    dvc_of_compress per frame == the oracle, with 1- and 3-channel decoded masks:
+    a 3-channel mask is grayed exactly first (of:147-149) — (1, 0, 0) grays to
+    0, so such a pixel must not gate its block."""
+    rng = np.random.default_rng(W * H + ch)
+    n = 7
+    frames = rng.integers(0, 256, (n, H, W, 3), dtype=np.uint8)
+    if ch == 1:
+        masks = ((rng.random((n, H, W)) < 0.01) * rng.integers(1, 256, (n, H, W))).astype(np.uint8)
+    else:
+        masks = np.zeros((n, H, W, 3), np.uint8)
+        sel = rng.random((n, H, W)) < 0.01
+        masks[sel] = rng.integers(0, 256, (int(sel.sum()), 3))
+        faint = rng.random((n, H, W)) < 0.02            # grays to 0: static
+        masks[faint] = (1, 0, 0)
+    c = gpu_lib._native.OFCompressor(W, H, max_batch=3)
+    got = c.run(frames, masks)
+    c.close()
+    gm = masks if ch == 1 else _gray(masks)
+    for t in range(n):
+        want = oracle_lib.of_compress(frames[t], gm[t], 100.0)
+        assert np.array_equal(got[t], want), t
+        assert np.array_equal(gpu_lib._native.of_compress(frames[t], gm[t], 100.0), want), t
+
+
+def test_compress_with_motion_dropin_chunks(gpu_lib, oracle_lib, tmp_path, monkeypatch):
+    """The drop-in's second pass in chunks (READ_AHEAD 4 over 11 frame pairs)
+    with a 3-channel mask video as VideoCapture decodes mask.mp4, at a size that
+    is not a multiple of 8: == the oracle per frame on the grayed mask; the mask
+    video being shorter ends the loop (of:144-145)."""
+    from dvc_amd import motion_compression_opt as M
+    monkeypatch.setattr(M, "READ_AHEAD", 4)
+    rng = np.random.default_rng(7)
+    W, H = 165, 99
+    frames = rng.integers(0, 256, (11, H, W, 3), dtype=np.uint8)
+    masks = np.zeros((10, H, W, 3), np.uint8)
+    for t in range(10):
+        y, x = rng.integers(0, H - 20), rng.integers(0, W - 30)
+        masks[t, y:y + 20, x:x + 30] = 255
+        masks[t, rng.random((H, W)) < 0.01] = (1, 0, 0)     # grays to 0
+    np.save(tmp_path / "in.npy", frames)
+    np.save(tmp_path / "mask.npy", masks)
+    n, total, avg = M.compress_with_motion(str(tmp_path / "in.npy"), str(tmp_path / "mask.npy"), str(tmp_path))
+    assert n == 10 and total > 0 and abs(avg - total / 10) < 1e-9
+    got = np.load(tmp_path / "compressed.npy")
+    gm = ((masks.astype(np.uint32) * np.array([1868, 9617, 4899])).sum(-1) + 8192 >> 14).astype(np.uint8)
+    for t in range(10):
+        assert np.array_equal(got[t], oracle_lib.of_compress(frames[t], gm[t], 100.0)), t

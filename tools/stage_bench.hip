@@ -53,13 +53,12 @@ int main(int argc, char** argv)
     CK(hipMalloc(&stats, 8 * 4 * 64));
     CK(hipMemset(acc, 0, N));
     dvc::CclBufs c{};
-    size_t sz[10];
+    size_t sz[dvc::CclBufs::NARR];
     dvc::CclBufs::sizes(g, n, sz);
-    void** ptrs[10] = {(void**)&c.mbits, (void**)&c.fbits, (void**)&c.rs, (void**)&c.re, (void**)&c.nfg,
-                       (void**)&c.fpar, (void**)&c.gpar, (void**)&c.gE, (void**)&c.area2, (void**)&c.kbits};
-    for (int i = 0; i < 10; ++i) CK(hipMalloc(ptrs[i], sz[i]));
+    void** ptrs[dvc::CclBufs::NARR];
+    c.ptrs(ptrs);
+    for (int i = 0; i < dvc::CclBufs::NARR; ++i) CK(hipMalloc(ptrs[i], sz[i]));
     CK(hipMemset(c.gpar, 0, sz[6]));
-    CK(hipMalloc(&c.rowb, dvc::CclBufs::rowb_bytes(g, n)));
     c.stats = stats;
     const int B = 4, NBX = (W + B - 1) / B, NBY = (H + B - 1) / B, SW = (NBX + 63) / 64, gs = (W + 3) & ~3;
     uint64_t *dblk, *rblk, *sbits;
