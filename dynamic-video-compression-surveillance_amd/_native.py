@@ -44,6 +44,7 @@ EXPORTS = [
     "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
     "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free", "dvc_yuv420_to_bgr", "dvc_bgr_to_i420",
     "dvc_copy_rate", "dvc_ofc_create", "dvc_ofc_run", "dvc_ofc_sync", "dvc_ofc_destroy",
+    "dvc_fd_set_state", "dvc_of_set_state",
 ]
 ABI_VERSION = 6
 MAX_BATCH = 512
@@ -162,6 +163,10 @@ def lib() -> ctypes.CDLL:
     L.dvc_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     L.dvc_fd_create.argtypes = [ctypes.POINTER(FdParams), ctypes.c_int, vp, ctypes.POINTER(vp)]
     L.dvc_fd_prime.argtypes = [vp, u8p, ctypes.c_size_t]
+    L.dvc_fd_set_state.argtypes = [vp, u8p, u8p]
+    L.dvc_fd_set_state.restype = ctypes.c_int
+    L.dvc_of_set_state.argtypes = [vp, u8p, u8p, ctypes.c_int]
+    L.dvc_of_set_state.restype = ctypes.c_int
     L.dvc_fd_step.argtypes = [vp, u8p, ctypes.c_size_t, u8p, u8p, u8p]
     L.dvc_fd_sync.argtypes = [vp]
     L.dvc_fd_get_stats.argtypes = [vp, ctypes.POINTER(FdStats)]

@@ -695,6 +695,35 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
     return DVC_OK;
 }
 
+// Resume a feed (checkpoint / resume): the state the reference
+// carries from frame to frame — the previous blurred gray (fd:77,93,133) and
+// the accumulated mask (fd:81,107), host H x W planes as dvc_fd_read_plane
+// exports them (DVC_PLANE_GRAY, DVC_PLANE_ACC). Like dvc_fd_prime it starts a
+// new run: counters and the odd-DCT stop are reset.
+int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
+{
+    if (!h || !prev_gray || !acc) return fail(DVC_E_INVALID, "NULL argument");
+    HIP_OK(hipSetDevice(h->device));
+    const size_t W = h->p.width, H = h->p.height;
+    HIP_OK(sync_all(h));  // no batch of a previous run may still be in flight
+    HIP_OK(wait_user(h));
+    for (Slot& s : h->slot) s.recorded = false;
+    for (Stage& s : h->stage) s.busy = false;
+    HIP_OK(hipMemcpy2DAsync(h->gray[h->gcur], h->gs, prev_gray, W, W, H, hipMemcpyHostToDevice, h->s_front));
+    // the acc rows have pitch AP; the padding of partial blocks stays 0 (create)
+    HIP_OK(hipMemcpy2DAsync(h->acc, h->AP, acc, W, W, H, hipMemcpyHostToDevice, h->s_front));
+    HIP_OK(hipMemsetAsync(h->stats, 0, 8 * 4 * 64, h->s_front));
+    HIP_OK(hipMemsetAsync(h->err, 0xff, 8, h->s_front));
+    HIP_OK(hipStreamSynchronize(h->s_front));
+    h->frames = 0;
+    h->seq = 0;
+    h->last_n = 0;
+    h->primed = true;
+    h->failed = false;
+    h->err_frame = 0;
+    return DVC_OK;
+}
+
 }  // extern "C"
 
 // Enqueue one batch i of n <= max_batch frames, slot S = i % 3 (j = i - 3 =

@@ -566,6 +566,71 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     return DVC_OK;
 }
 
+// Resume a feed (checkpoint / resume) from the state the
+// reference carries across frames: the previous gray (of:60,101) and the raw
+// |flow| masks of the last n frames, oldest first (the deque, of:61,84;
+// nonzero = motion; n > window keeps the newest window). Host planes of H x W
+// bytes, as dvc_of_read_plane exports them (DVC_OF_PLANE_GRAY, _RAW). The
+// previous frame's pyramid is rebuilt from the gray exactly: a BGR frame with
+// B = G = R = gray grays back to itself ((1868 + 9617 + 4899) * g + 2^13 >> 14
+// = g), so the prime path runs on it. Counters are reset, as by dvc_of_prime.
+int dvc_of_set_state(dvc_of* h, const uint8_t* prev_gray, const uint8_t* raw_masks, int n)
+{
+    if (!h || !prev_gray || (n > 0 && !raw_masks) || n < 0) return fail(DVC_E_INVALID, "NULL argument / bad count");
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(of_sync_all(h));
+    HIP_OK(of_wait_user(h));
+    const size_t W = h->p.width, H = h->p.height, WW = h->g.WW, window = (size_t)h->p.window;
+    if ((size_t)n > window) {
+        raw_masks += ((size_t)n - window) * W * H;
+        n = (int)window;
+    }
+    // the previous frame as gray-replicated BGR rows of ip, through the prime path
+    std::vector<uint8_t> bgr((size_t)h->ip * H, 0);
+    for (size_t y = 0; y < H; ++y)
+        for (size_t x = 0; x < W; ++x) {
+            const uint8_t g = prev_gray[y * W + x];
+            uint8_t* p = &bgr[y * h->ip + 3 * x];
+            p[0] = p[1] = p[2] = g;
+        }
+    uint8_t* d = nullptr;
+    HIP_OK(of_alloc(h, &d, bgr.size()));
+    HIP_OK(hipMemcpy(d, bgr.data(), bgr.size(), hipMemcpyHostToDevice));
+    // frames 1..n are the window's masks; the previous frame is a = n
+    std::vector<uint64_t> bits(H * WW * std::max(n, 1), 0);
+    std::vector<uint8_t> cnt(64 * H * WW, 0);   // bytes, rows of 64 WW (k_vote's counters)
+    for (int k = 0; k < n; ++k)
+        for (size_t y = 0; y < H; ++y)
+            for (size_t x = 0; x < W; ++x)
+                if (raw_masks[((size_t)k * H + y) * W + x]) {
+                    bits[((size_t)k * H + y) * WW + x / 64] |= 1ull << (x % 64);
+                    cnt[y * 64 * WW + x]++;
+                }
+    HIP_OK(hipMemsetAsync(h->b.mring, 0, 8 * H * WW * h->g.RB, h->stream));
+    for (int k = 0; k < n; ++k)
+        HIP_OK(hipMemcpyAsync(h->b.mring + (size_t)((k + 1) % h->g.RB) * H * WW, bits.data() + (size_t)k * H * WW,
+                              8 * H * WW, hipMemcpyHostToDevice, h->stream));
+    HIP_OK(hipMemcpyAsync(h->b.cnt, cnt.data(), cnt.size(), hipMemcpyHostToDevice, h->stream));
+    for (OfSlot& sl : h->slot) sl.recorded = false;
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, h->ip, (size_t)h->ip * H, n, 1, h->stream));
+    HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
+    HIP_OK(hipMemsetAsync(h->b.scan_abort, 0, 4, h->stream));
+    HIP_OK(hipStreamSynchronize(h->stream));
+    // the temporary frame is released now (no kernel reads it any more)
+    for (size_t i = 0; i < h->dev.size(); ++i)
+        if (h->dev[i] == d) {
+            (void)hipFree(d);
+            h->dev.erase(h->dev.begin() + (long)i);
+            break;
+        }
+    h->seq = 0;
+    h->a_next = n + 1;
+    h->frames = 0;
+    h->last_n = 0;
+    h->primed = true;
+    return DVC_OK;
+}
+
 }  // extern "C"
 
 static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n, uint8_t* mask, size_t mstride,

@@ -58,6 +58,12 @@ __device__ __forceinline__ void ld10(const float* p, float* o)
     o[9] = c.y;
 }
 
+// FarnebackUpdateMatrices' border weights {0.14, 0.14, 0.4472, 0.4472, 0.4472}
+// for distance d (0..4) from the image edge, as a select instead of a memory
+// table (a table load is a vector memory op: waiting for it waits for every
+// prefetch issued before it)
+__device__ __forceinline__ float border_w(int d) { return d < 2 ? 0.14f : 0.4472f; }
+
 namespace {
 
 constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
@@ -358,7 +364,6 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
     const float* __restrict__ R0 = A.lv.R + (size_t)ring(a - 1, g.RS) * lvpx * 5;
     const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
     const float* src = A.src ? A.src + (size_t)t * (A.src_mode == 1 ? (size_t)A.sw * A.sh : lvpx) * 2 : nullptr;
-    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
 
     // ---- FarnebackUpdateMatrices over tile + halo (oc_update_matrices).
     // Positions in groups of MQ per thread: every address is clamped into the
@@ -459,8 +464,8 @@ __device__ __forceinline__ void flow_tile(const FlowArgs& A, double* lds_d)
             R23 = R23 + ((f32x2){R45.x, r6} * (f32x2)dy + (f32x2){r6, R45.y} * (f32x2)dx);
             if constexpr (!INT) {
                 if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
-                    const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
-                                        (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+                    const float scale = (x < 5 ? border_w(x) : 1.f) * (x >= w - 5 ? border_w(w - x - 1) : 1.f) *
+                                        (y < 5 ? border_w(y) : 1.f) * (y >= h - 5 ? border_w(h - y - 1) : 1.f);
                     R23 = R23 * (f32x2)scale;
                     R45 = R45 * (f32x2)scale;
                     r6 *= scale;
@@ -713,7 +718,6 @@ template <int MQ>
 __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& P, float* sM)
 {
     const int w = A.lv.w, h = A.lv.h;
-    static const float border[5] = {0.14f, 0.14f, 0.4472f, 0.4472f, 0.4472f};
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
         if (!P.ok[u]) continue;
@@ -743,8 +747,8 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
         R23 = (R0_01 - R23) * (f32x2)0.5f;
         R23 = R23 + ((f32x2){R45.x, r6} * (f32x2)dy + (f32x2){r6, R45.y} * (f32x2)dx);
         if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
-            const float scale = (x < 5 ? border[x] : 1.f) * (x >= w - 5 ? border[w - x - 1] : 1.f) *
-                                (y < 5 ? border[y] : 1.f) * (y >= h - 5 ? border[h - y - 1] : 1.f);
+            const float scale = (x < 5 ? border_w(x) : 1.f) * (x >= w - 5 ? border_w(w - x - 1) : 1.f) *
+                                (y < 5 ? border_w(y) : 1.f) * (y >= h - 5 ? border_w(h - y - 1) : 1.f);
             R23 = R23 * (f32x2)scale;
             R45 = R45 * (f32x2)scale;
             r6 *= scale;
@@ -890,6 +894,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         STAMP(0);
         mat_stage2<MQ>(A, R0, R1, P);   // 1'. block b+1: R0 and the displaced R1 loads
         set_block(Q, y0 + 2 * RB);      //     block b+2: positions and flow loads
+        STAMP(6);
         // 2. vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
@@ -902,6 +907,24 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             }
             // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0), stepped
             int sa = (y0 + m) % RING, sb = y0 - m - 1 >= 0 ? (y0 - m - 1) % RING : 0;
+            if (nrow == RB && y0 - m - 1 >= 0 && y0 + RB - 1 + m <= h - 1) {
+                // a block with no clamped row: all 2 RB ring loads issued before
+                // the first add of the chain (one LDS round trip, not RB)
+                float va[RB], vb[RB];
+#pragma unroll
+                for (int i = 0; i < RB; ++i) {
+                    const int ta = sa + i < RING ? sa + i : sa + i - RING;
+                    const int tb = sb + i < RING ? sb + i : sb + i - RING;
+                    va[i] = sM[(ta * NC + j) * 5 + c];
+                    vb[i] = sM[(tb * NC + j) * 5 + c];
+                }
+#pragma unroll
+                for (int i = 0; i < RB; ++i) {
+                    vsum[k] += (double)(va[i] - vb[i]);
+                    sV[i * VS + ch] = vsum[k];
+                }
+                continue;
+            }
             for (int i = 0; i < nrow; ++i) {
                 const int y = y0 + i;
                 const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
@@ -912,6 +935,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                 if (y - m - 1 >= 0) sb = sb + 1 == RING ? 0 : sb + 1;
             }
         }
+        STAMP(7);
         __syncthreads();   // the M ring is free from here: no reader until the next block's step 2
         STAMP(1);
         if (tid < 64) {
@@ -1014,8 +1038,8 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     }
 }
 
-template <int SW, int RB, int NT, int SMODE, int MM>
-__global__ void __launch_bounds__(NT, NT == 512 ? 4 : 2) k_flow_scan(ScanArgs S)
+template <int SW, int RB, int NT, int SMODE, int MM, int OCC>
+__global__ void __launch_bounds__(NT, OCC) k_flow_scan(ScanArgs S)
 {
     static_assert(SW == 64, "a wave's mask ballot is one 64-column mask word");
     extern __shared__ __attribute__((aligned(16))) double lds_s[];
@@ -1649,13 +1673,17 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
             if (g.sliding) {   // OpenCV's running box sums: strip wavefront
-                // strips of 64 columns x blocks of 12 rows (box radius m <= 4: winsize <= 9,
-                // the reference's) or 8, 512 threads (DVC_OF_SCAN=256: 256 threads)
+                // strips of 64 columns x blocks of RB rows, NT threads, OCC waves per
+                // SIMD (register budget); DVC_OF_SCAN=<index> picks a variant of the
+                // box radius m <= 4 table (winsize <= 9, the reference's) for A/B runs
+                struct Cfg { int nt, rb; };
+                static const Cfg cfg4[] = {{512, 12}, {512, 6}, {256, 6}, {384, 6}, {256, 8}, {512, 8}};
                 static const int scan_cfg = [] {
                     const char* e = getenv("DVC_OF_SCAN");
-                    return e && !strcmp(e, "256") ? 1 : 0;
+                    const int v = e ? atoi(e) : 0;
+                    return v >= 0 && v < 6 ? v : 0;
                 }();
-                const int sw = 64, rb = g.m <= 4 ? 12 : 8;
+                const int sw = 64, rb = g.m <= 4 ? cfg4[scan_cfg].rb : 8;
                 ScanArgs S{};
                 S.f = A;
                 S.S = (L.w + sw - 1) / sw;
@@ -1676,17 +1704,25 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
                 const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
-                switch (scan_cfg * 4 + (rb == 12) * 2 + (S.f.src_mode == 2)) {
-#define DVC_SCAN_CASE(i, NTv, RBv, SM, MMv) \
-    case i: hipLaunchKernelGGL((k_flow_scan<64, RBv, NTv, SM, MMv>), dim3(grid_s), dim3(NTv), lds_b, s, S); break;
-                    DVC_SCAN_CASE(0, 512, 8, 0, OF_MAX_BOX_M)
-                    DVC_SCAN_CASE(1, 512, 8, 2, OF_MAX_BOX_M)
-                    DVC_SCAN_CASE(2, 512, 12, 0, 4)
-                    DVC_SCAN_CASE(3, 512, 12, 2, 4)
-                    DVC_SCAN_CASE(4, 256, 8, 0, OF_MAX_BOX_M)
-                    DVC_SCAN_CASE(5, 256, 8, 2, OF_MAX_BOX_M)
-                    DVC_SCAN_CASE(6, 256, 12, 0, 4)
-                    DVC_SCAN_CASE(7, 256, 12, 2, 4)
+                const int sm2 = S.f.src_mode == 2;
+                const int sel = g.m <= 4 ? 2 + 2 * scan_cfg + sm2 : sm2;
+                switch (sel) {
+#define DVC_SCAN_CASE(i, NTv, RBv, SM, MMv, OCCv) \
+    case i: hipLaunchKernelGGL((k_flow_scan<64, RBv, NTv, SM, MMv, OCCv>), dim3(grid_s), dim3(NTv), lds_b, s, S); break;
+                    DVC_SCAN_CASE(0, 512, 8, 0, OF_MAX_BOX_M, 2)
+                    DVC_SCAN_CASE(1, 512, 8, 2, OF_MAX_BOX_M, 2)
+                    DVC_SCAN_CASE(2, 512, 12, 0, 4, 4)
+                    DVC_SCAN_CASE(3, 512, 12, 2, 4, 4)
+                    DVC_SCAN_CASE(4, 512, 6, 0, 4, 6)
+                    DVC_SCAN_CASE(5, 512, 6, 2, 4, 6)
+                    DVC_SCAN_CASE(6, 256, 6, 0, 4, 4)
+                    DVC_SCAN_CASE(7, 256, 6, 2, 4, 4)
+                    DVC_SCAN_CASE(8, 384, 6, 0, 4, 6)
+                    DVC_SCAN_CASE(9, 384, 6, 2, 4, 6)
+                    DVC_SCAN_CASE(10, 256, 8, 0, 4, 4)
+                    DVC_SCAN_CASE(11, 256, 8, 2, 4, 4)
+                    DVC_SCAN_CASE(12, 512, 8, 0, 4, 6)
+                    DVC_SCAN_CASE(13, 512, 8, 2, 4, 6)
 #undef DVC_SCAN_CASE
                 }
             } else if (g.m == 4) {

@@ -115,6 +115,16 @@ class FDWorker:
             f = B.host_in(frame, self._fshape, "frame")
             N.check(self._lib.dvc_fd_prime(self._h, f.ctypes.data, self._pitch))
 
+    def set_state(self, prev_gray, acc) -> None:
+        """Resume instead of :meth:`prime` (dvc_fd_set_state): the previous
+        blurred gray and the accumulated mask (fd:107,133), H x W uint8 each —
+        what :meth:`plane` exports as PLANE_GRAY / PLANE_ACC."""
+        g = np.ascontiguousarray(prev_gray, dtype=np.uint8)
+        a = np.ascontiguousarray(acc, dtype=np.uint8)
+        if g.shape != (self.H, self.W) or a.shape != (self.H, self.W):
+            raise ValueError(f"state planes must be ({self.H}, {self.W})")
+        N.check(self._lib.dvc_fd_set_state(self._h, g.ctypes.data, a.ctypes.data))
+
     def step(self, frame, overlay=None, compressed=None, acc=None, want=("overlay", "compressed")):
         """fd:91-133 for one frame.
 

@@ -85,6 +85,19 @@ class OFWorker:
             f = B.host_in(frame, self._fshape, "frame")
             N.check(self._lib.dvc_of_prime(self._h, f.ctypes.data, self._pitch))
 
+    def set_state(self, prev_gray, raw_masks) -> None:
+        """Resume instead of :meth:`prime` (dvc_of_set_state): the previous gray
+        (H x W, of:101) and the raw |flow| masks of the last frames, oldest
+        first ((n, H, W), of:84) — :meth:`plane` with OF_PLANE_GRAY / _RAW
+        exports them."""
+        g = np.ascontiguousarray(prev_gray, dtype=np.uint8)
+        m = np.ascontiguousarray(raw_masks, dtype=np.uint8)
+        if m.ndim == 2:
+            m = m[None]
+        if g.shape != (self.H, self.W) or m.shape[1:] != (self.H, self.W):
+            raise ValueError(f"state planes must be ({self.H}, {self.W})")
+        N.check(self._lib.dvc_of_set_state(self._h, g.ctypes.data, m.ctypes.data if len(m) else None, len(m)))
+
     def step(self, frame, mask=None, compressed=None, want=("mask", "compressed")):
         """of:70-101 + of:151-183 for one frame. Host mode returns ``(mask,
         compressed)`` (H x W {0,255} and H x W x 3); device mode writes into the

@@ -204,6 +204,13 @@ int dvc_fd_create(const dvc_fd_params* params, int device, void* hip_stream, dvc
  * and clears a DVC_E_ODD_DCT stop. Frames are src_width x src_height. */
 int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch);
 
+/* Resume a feed instead of priming it (checkpoint / resume): the state the
+ * reference carries across frames — the previous blurred gray (fd:93,133)
+ * and the accumulated mask (fd:107) — as host H*W planes (dvc_fd_read_plane's
+ * DVC_PLANE_GRAY and DVC_PLANE_ACC export them). The next step continues
+ * exactly as the uninterrupted run; counters restart as after dvc_fd_prime. */
+int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc);
+
 /* One frame of the hot loop, fd:91-133: gray, GaussianBlur 5x5, absdiff,
  * threshold, findContours/contourArea/drawContours filter, dilate, addWeighted,
  * red overlay (fd:110-111) and the mask-gated block DCT quantisation with the
@@ -330,6 +337,13 @@ int dvc_of_create(const dvc_of_params* params, int device, void* hip_stream, dvc
 
 /* Frame 0: gray (of:60) and its pyramid; the vote window is emptied (of:61). */
 int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch);
+
+/* Resume a feed instead of priming it (checkpoint / resume): the previous gray
+ * (of:101) and the raw |flow| > thr masks of the last n frames, oldest first
+ * (the deque of:84; only the newest `window` are kept), host H*W planes as
+ * dvc_of_read_plane exports them (DVC_OF_PLANE_GRAY, DVC_OF_PLANE_RAW). The
+ * next step continues exactly as the uninterrupted run; counters restart. */
+int dvc_of_set_state(dvc_of* h, const uint8_t* prev_gray, const uint8_t* raw_masks, int n);
 
 /* One frame of the fused worker: gray, calcOpticalFlowFarneback(prev, gray),
  * |flow| > thr, windowed vote, close/open, rectangle mask (of:70-97), and the

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 import dvc_amd  # noqa: E402
 from dvc_amd.synthetic import SyntheticClip  # noqa: E402
 
-W, H, n = 1920, 1080, 16
+W, H, n = 1920, 1080, int(os.environ.get("DVC_STAMP_FRAMES", "16"))
 clip = SyntheticClip(W, H, seed=0)
 fr = torch.from_numpy(np.stack([clip.frame(i) for i in range(n + 1)])).cuda()
 w = dvc_amd.OFWorker(W, H, device=0, device_ptrs=True, max_batch=n)
@@ -38,6 +38,10 @@ names = ["vertical", "wait", "chain/M", "barrier", "solve"]
 for i, nm in enumerate(names):
     print(f"{nm:10s} median {np.median(ph[:, :, i]):7.2f} us  p90 {np.percentile(ph[:, :, i], 90):7.2f}")
 print(f"step total median {np.median(np.sum(ph, axis=2)):.2f} us")
+sub = {"prefetch issue (0->6)": (0, 6), "vertical sums (6->7)": (6, 7), "barrier A (7->1)": (7, 1)}
+for nm, (i, j) in sub.items():
+    d = (a[:, :, j] - a[:, :, i]) / 2.1e3
+    print(f"  {nm:24s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}")
 print("strip 0 block starts (us):", np.round(rel[0, :6, 0], 2))
 print("strip 15 block starts (us):", np.round(rel[15, :6, 0], 2))
 print("last strip end:", round(rel[S - 1, B - 1, 5], 1), "us; strip starts:", np.round(rel[:, 0, 0], 1)[:10])
