@@ -261,14 +261,34 @@ static bool of_direct(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fs
     return pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
 
-// The BGR frames the kernels read for a batch in slot S: the caller's device
-// frames in place, or (re-pitch needed, or 4:2:0 surfaces) converted / copied
-// into S.fin on stream `st` once the slot's previous batch is done with it.
+// Can k_of_front0 / k_of_out read these 4:2:0 surfaces in place? Dword luma
+// rows (pitch % 4 == 0, so rows reach whole quads), aligned base and stride.
+// DVC_OF_YUV_DIRECT=0 forces the staged conversion (A/B).
+static bool of_direct_yuv(const uint8_t* p, size_t pitch, size_t fstride, int n)
+{
+    static const int on = [] { const char* e = getenv("DVC_OF_YUV_DIRECT"); return e ? atoi(e) : 1; }();
+    return on && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
+}
+
+// The frames the kernels read for a batch in slot S: the caller's device
+// frames in place (BGR rows the kernels can read, or 4:2:0 surfaces converted
+// per pixel as they load: *sf says which), or (re-pitch needed, surfaces not
+// readable in place) converted / copied into S.fin on stream `st` once the
+// slot's previous batch is done with it.
 static int of_stage(dvc_of* h, OfSlot& S, const uint8_t* d, int dp, size_t fstride, int n, int crows, hipStream_t st,
-                    const uint8_t** kd, int* kp, size_t* kfs)
+                    const uint8_t** kd, int* kp, size_t* kfs, dvc::SrcFmt* sf)
 {
     const size_t W = h->p.width, H = h->p.height, FS = (size_t)h->ip * H;
+    *sf = dvc::SrcFmt{DVC_FMT_BGR, 0, 0, 0};
     if (h->fmt == DVC_FMT_BGR && of_direct(h, d, (size_t)dp, fstride, n)) {
+        *kd = d;
+        *kp = dp;
+        *kfs = fstride;
+        return DVC_OK;
+    }
+    if (h->fmt != DVC_FMT_BGR && of_direct_yuv(d, (size_t)dp, fstride, n)) {
+        const dvc::YuvLayout L = dvc::yuv_layout(d, dp, h->fmt, crows, fstride);
+        *sf = dvc::SrcFmt{h->fmt, L.uoff, L.voff, L.cpitch};
         *kd = d;
         *kp = dp;
         *kfs = fstride;
@@ -547,9 +567,10 @@ int dvc_of_prime(dvc_of* h, const uint8_t* bgr, size_t pitch)
     const uint8_t* kd = nullptr;
     int kp = 0;
     size_t kfs = 0;
-    int rc = of_stage(h, h->slot[0], d, dp, 0, 1, crows, h->stream, &kd, &kp, &kfs);
+    dvc::SrcFmt sf{};
+    int rc = of_stage(h, h->slot[0], d, dp, 0, 1, crows, h->stream, &kd, &kp, &kfs, &sf);
     if (rc) return rc;
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, kd, kp, kfs, 0, 1, h->stream));   // of:60
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, kd, kp, kfs, sf, 0, 1, h->stream));   // of:60
     HIP_OK(hipMemsetAsync(h->b.mring, 0, 8 * H * WW * h->g.RB, h->stream));            // of:61 deque()
     HIP_OK(hipMemsetAsync(h->b.cnt, 0, 64 * H * WW, h->stream));
     HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
@@ -612,7 +633,7 @@ int dvc_of_set_state(dvc_of* h, const uint8_t* prev_gray, const uint8_t* raw_mas
                               8 * H * WW, hipMemcpyHostToDevice, h->stream));
     HIP_OK(hipMemcpyAsync(h->b.cnt, cnt.data(), cnt.size(), hipMemcpyHostToDevice, h->stream));
     for (OfSlot& sl : h->slot) sl.recorded = false;
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, h->ip, (size_t)h->ip * H, n, 1, h->stream));
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, h->ip, (size_t)h->ip * H, dvc::SrcFmt{}, n, 1, h->stream));
     HIP_OK(hipMemsetAsync(h->b.stats, 0, 8 * 4 * 64, h->stream));
     HIP_OK(hipMemsetAsync(h->b.scan_abort, 0, 4, h->stream));
     HIP_OK(hipStreamSynchronize(h->stream));
@@ -652,18 +673,19 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
         return v;
     }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
-    {   // 4:2:0 surfaces -> BGR (of:66,145), or re-pitched BGR, in the slot's
-        // frames, read by the pyramid and by k_of_out
+    dvc::SrcFmt sf{};
+    {   // 4:2:0 surfaces read in place, or -> BGR (of:66,145) / re-pitched BGR in
+        // the slot's frames, read by the pyramid and by k_of_out
         const uint8_t* kd = nullptr;
         int kp = 0;
         size_t kfs = 0;
-        int rc = of_stage(h, S, d, dp, fstride, n, crows, h->s_pyr, &kd, &kp, &kfs);
+        int rc = of_stage(h, S, d, dp, fstride, n, crows, h->s_pyr, &kd, &kp, &kfs, &sf);
         if (rc) return rc;
         d = kd;
         dp = kp;
         fstride = kfs;
     }
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, a0, n, h->s_pyr));
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, sf, a0, n, h->s_pyr));
     HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
     HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_pyr, 0));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_mask, 0));
@@ -695,6 +717,7 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     o.quant = h->p.quant;
     o.qinv = 1.0 / (double)h->p.quant;
     o.M = h->M;
+    o.sf = sf;
     if (!(skip & 8)) HIP_OK(dvc::of_launch_out(h->g, h->b, o, n, h->s_mask));
     HIP_OK(hipEventRecord(S.ev_mask, h->s_mask));
     S.recorded = true;

@@ -114,12 +114,17 @@ struct OfOutArgs {
     float quant;
     double qinv;           // RN53(1 / (double)quant), see div_rn
     DctMat M;              // 8x8 orthonormal DCT-II basis
+    SrcFmt sf;             // bgr: packed BGR (fmt 0) or 4:2:0 surfaces read in place (of_launch_pyramid)
 };
 
 // gray + pyramid + polynomial expansion of frames a0 .. a0+n-1 (their BGR at
 // bgr + t*fstride) into the R rings; gray kept in b.gray.
+// sf: how the frames are read — packed BGR rows of `pitch` (sf.fmt = BGR), or
+// 4:2:0 decoder surfaces read in place (luma rows of `pitch`, chroma at
+// sf.uoff / sf.voff, rows of sf.cpitch; fd_kernels.h SrcFmt), converted as
+// cvtColor YUV2BGR per pixel as they load (what cap.read() returns, of:66)
 hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
-                             size_t fstride, long long a0, int n, hipStream_t s);
+                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s);
 // Farneback levels k_hi down to k_lo (L..0 in total, coarse to fine) for frames
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,

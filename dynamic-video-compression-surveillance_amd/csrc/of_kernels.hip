@@ -34,8 +34,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../include/dvc.h"
 #include "dvc_device.h"
 #include "of_kernels.h"
+#include "yuv_px.h"
 
 namespace dvc {
 
@@ -155,10 +157,35 @@ __device__ __forceinline__ void poly_tile(const float* sI, float* sv, const Poly
 // (PN+1) halo, the level-0 smoothing (GaussianBlur 3x3, sigma 0 -> taps
 // (0.25, 0.5, 0.25), BORDER_REFLECT_101) over tile + PN halo, then the
 // polynomial expansion. blockIdx.z = frame of the batch.
-template <int PN, bool INT>
+// Gray of 4 px at column px of row y of frame f: 12 packed BGR bytes, or a
+// 4:2:0 quad — its luma dword and chroma (I420: a u16 of U and of V; NV12: the
+// UVUV dword) through cvtColor YUV2BGR (yuv_px.h), then BGR2GRAY (of:71).
+template <int FMT>
+__device__ __forceinline__ uint32_t of_quad_gray(const uint8_t* f, int y, int px, int pitch, const SrcFmt& sf)
+{
+    if constexpr (FMT == DVC_FMT_BGR) {
+        const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)y * pitch + 3 * px);
+        return gray4_dot(v.x, v.y, v.z);
+    } else {
+        const uint32_t y4 = *reinterpret_cast<const uint32_t*>(f + (size_t)y * pitch + px);
+        const uint8_t* c = f + sf.uoff + (size_t)(y >> 1) * sf.cpitch;
+        uint32_t o[3];
+        if constexpr (FMT == DVC_FMT_NV12) {
+            const uint32_t uv = *reinterpret_cast<const uint32_t*>(c + px);
+            yuvpx::yuv4_bgr(y4, uv & 255, (uv >> 8) & 255, (uv >> 16) & 255, uv >> 24, o);
+        } else {
+            const uint32_t u = *reinterpret_cast<const uint16_t*>(c + (px >> 1));
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(c + (sf.voff - sf.uoff) + (px >> 1));
+            yuvpx::yuv4_bgr(y4, u & 255, v & 255, u >> 8, v >> 8, o);
+        }
+        return gray4_dot(o[0], o[1], o[2]);
+    }
+}
+
+template <int PN, bool INT, int FMT>
 __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, uint8_t* __restrict__ gray_out,
-                                            const uint8_t* __restrict__ bgr, int pitch, size_t fstride, long long a0,
-                                            float* sg, float* sI, float* sv)
+                                            const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
+                                            const SrcFmt& sf, long long a0, float* sg, float* sI, float* sv)
 {
     // gray tile: rows y0-HG .., columns from x0-GX in whole 4-px quads (GX = 8 >= HG
     // keeps each quad's 12 BGR bytes 4-byte aligned: x0 % 64 == 0, pitch % 4 == 0)
@@ -177,8 +204,7 @@ __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, ui
         // (pitch >= 3 * roundup(W, 4)), its gray values land in the gray rows'
         // padding (GP) and in LDS columns the clamped / reflected taps never read
         if (!INT && (y < 0 || y >= H || px < 0 || px >= W)) continue;
-        const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)y * pitch + 3 * px);
-        const uint32_t gq = gray4_dot(v.x, v.y, v.z);   // of:71 BGR2GRAY of 4 px
+        const uint32_t gq = of_quad_gray<FMT>(f, y, px, pitch, sf);   // of:71 BGR2GRAY of 4 px
         *reinterpret_cast<float4*>(sg + i * GW + 4 * q) =
             make_float4((float)(gq & 255), (float)((gq >> 8) & 255), (float)((gq >> 16) & 255), (float)(gq >> 24));
         if (i >= HG && i < HG + PT_H && px >= x0 && px < x0 + PT_W)
@@ -213,10 +239,10 @@ __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, ui
 
 // Interior tiles (the tile with its GX-px quad pad and HG-row halo inside the
 // frame) take the unclamped form: the same arithmetic on the same values.
-template <int PN>
+template <int PN, int FMT>
 __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* __restrict__ gray_out,
                                                    const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
-                                                   long long a0)
+                                                   SrcFmt sf, long long a0)
 {
     constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG;
     constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
@@ -225,8 +251,8 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
     __shared__ float sv[PT_H * IW * 3];
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     const bool interior = x0 >= GX && x0 + PT_W + GX <= g.W && y0 >= HG && y0 + PT_H + HG <= g.H;   // uniform
-    if (interior) front0_tile<PN, true>(g, lv, gray_out, bgr, pitch, fstride, a0, sg, sI, sv);
-    else front0_tile<PN, false>(g, lv, gray_out, bgr, pitch, fstride, a0, sg, sI, sv);
+    if (interior) front0_tile<PN, true, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sg, sI, sv);
+    else front0_tile<PN, false, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sg, sI, sv);
 }
 
 // ----------------------------------------------------------- level k > 0 ----
@@ -1421,7 +1447,31 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
     {
         const uint8_t* src8 = o.bgr + (size_t)t * o.fstride + (size_t)(act ? y : 0) * o.pitch + 3 * (act ? bx : 0);
         uint32_t px[6];
-        if (np == 8) {   // 24 bytes, dword aligned (pitch, fstride % 4 == 0; 3 bx % 24 == 0)
+        if (o.sf.fmt != DVC_FMT_BGR) {
+            // a 4:2:0 surface read in place: the 8 px's luma (2 dwords, aligned:
+            // pitch % 4 == 0, bx % 8 == 0) and the 4 chroma pairs of their 2x2
+            // quads, cvtColor YUV2BGR (yuv_px.h) into the 24 BGR bytes
+            const uint8_t* f = o.bgr + (size_t)t * o.fstride;
+            const uint8_t* yr = f + (size_t)(act ? y : 0) * o.pitch + (act ? bx : 0);
+            const uint8_t* c = f + o.sf.uoff + (size_t)((act ? y : 0) >> 1) * o.sf.cpitch;
+            const size_t dv = o.sf.voff - o.sf.uoff;
+            const int cst = o.sf.fmt == DVC_FMT_NV12 ? 2 : 1;   // bytes between chroma samples
+            const uint8_t* cu = c + (size_t)(act ? bx : 0) / 2 * cst;
+            uint32_t y8[2] = {0, 0};
+            int us[4] = {0, 0, 0, 0}, vs[4] = {0, 0, 0, 0};
+            if (np == 8) {
+                y8[0] = reinterpret_cast<const uint32_t*>(yr)[0];
+                y8[1] = reinterpret_cast<const uint32_t*>(yr)[1];
+            } else {
+                for (int k = 0; k < np; ++k) y8[k >> 2] |= (uint32_t)yr[k] << (8 * (k & 3));
+            }
+            for (int k = 0; k < (np + 1) / 2; ++k) {   // sides even (4:2:0): whole pairs
+                us[k] = cu[k * cst];
+                vs[k] = cu[dv + (size_t)k * cst];
+            }
+            yuvpx::yuv4_bgr(y8[0], us[0], vs[0], us[1], vs[1], px);
+            yuvpx::yuv4_bgr(y8[1], us[2], vs[2], us[3], vs[3], px + 3);
+        } else if (np == 8) {   // 24 bytes, dword aligned (pitch, fstride % 4 == 0; 3 bx % 24 == 0)
             const uint32_t* src = reinterpret_cast<const uint32_t*>(src8);
 #pragma unroll
             for (int d = 0; d < 6; ++d) px[d] = src[d];
@@ -1580,14 +1630,21 @@ static long long reduce_frame(const OfGeom& g, long long a0)
 }
 
 hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
-                             size_t fstride, long long a0, int n, hipStream_t s)
+                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s)
 {
     a0 = reduce_frame(g, a0);
     if (n <= 0) return hipSuccess;
     {
         dim3 grid((g.W + PT_W - 1) / PT_W, (g.H + PT_H - 1) / PT_H, n);
-        if (g.pc.n == 5) hipLaunchKernelGGL(k_of_front0<5>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
-        else hipLaunchKernelGGL(k_of_front0<7>, grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, a0);
+#define DVC_FRONT0(PNv, FMTv) \
+    hipLaunchKernelGGL((k_of_front0<PNv, FMTv>), grid, dim3(256), 0, s, g, lv[0], b.gray, bgr, pitch, fstride, sf, a0)
+        const bool p5 = g.pc.n == 5;
+        switch (sf.fmt) {
+        case DVC_FMT_I420: if (p5) DVC_FRONT0(5, DVC_FMT_I420); else DVC_FRONT0(7, DVC_FMT_I420); break;
+        case DVC_FMT_NV12: if (p5) DVC_FRONT0(5, DVC_FMT_NV12); else DVC_FRONT0(7, DVC_FMT_NV12); break;
+        default: if (p5) DVC_FRONT0(5, DVC_FMT_BGR); else DVC_FRONT0(7, DVC_FMT_BGR); break;
+        }
+#undef DVC_FRONT0
     }
     for (int k = 1; k <= g.L; ++k) {
         hipLaunchKernelGGL(k_pyr_h, dim3(g.H, n), dim3(256), (size_t)g.GP, s, g, lv[k], b.gray);

@@ -306,3 +306,46 @@ def test_fd_i420_outputs_refused_for_partial_blocks(gpu_lib):
         with pytest.raises(DvcError) as ei:
             gpu_lib.FDWorker(W, H, device=0, out_format="I420", block_size=b)
         assert ei.value.code == DVC_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("fmt,W,H,pitch,crows,batch", [
+    ("I420", 320, 176, 384, 184, 3),    # padded decoder surface, read in place by k_of_front0 / k_of_out
+    ("NV12", 642, 362, 648, 368, 4),    # W % 4 = 2: partial quad and partial 8x8 blocks, in place
+    ("I420", 320, 176, 322, 176, 2),    # pitch % 4 != 0: converted into staging frames instead
+])
+def test_of_yuv_surfaces(gpu_lib, oracle_lib, fmt, W, H, pitch, crows, batch):
+    """OF fed 4:2:0 decoder surfaces in HBM (of:66,145: cap.read()): the kernels
+    convert per pixel as they load (cvtColor YUV2BGR) when the rows allow it,
+    else through the staged conversion; masks and compressed frames equal the
+    oracle worker on the oracle-converted BGR frames either way."""
+    import torch
+    from dvc_amd.synthetic import clip
+    n = 6
+    frames = clip(W, H, n, seed=W + 1, n_objects=3)
+    i420 = _i420_frames(oracle_lib, frames)
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    ref = oracle_lib.OracleOF(W, H)
+    ref.prime(bgr[0])
+    outs = [ref.step(f)[:2] for f in bgr[1:]]
+    ref.close()
+    surf = np.stack([_surface(f if fmt == "I420" else _nv12(f, H, W), H, W, fmt, pitch, crows) for f in i420])
+    d = torch.from_numpy(surf).cuda()
+    mk = torch.empty((n - 1, H, W), dtype=torch.uint8, device="cuda")
+    cp = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda")
+    N = gpu_lib._native
+    p = gpu_lib.of.derive_of_params(W, H, flags=N.DVC_FLAG_DEVICE_PTRS, in_format=fmt, chroma_rows=crows)
+    p.max_batch = batch
+    L = N.lib()
+    h = ctypes.c_void_p()
+    N.check(L.dvc_of_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+    try:
+        N.check(L.dvc_of_prime(h, d[0].data_ptr(), pitch))
+        N.check(L.dvc_of_step_batch(h, d[1].data_ptr(), pitch, surf[0].nbytes, n - 1, mk.data_ptr(), H * W,
+                                    cp.data_ptr(), 3 * H * W))
+        N.check(L.dvc_of_sync(h))
+    finally:
+        L.dvc_of_destroy(h)
+    mk, cp = mk.cpu().numpy(), cp.cpu().numpy()
+    for t, (rm, rc) in enumerate(outs):
+        assert np.array_equal(mk[t], rm), f"mask differs at frame {t + 1}"
+        assert np.array_equal(cp[t], rc), f"compressed differs at frame {t + 1}"
