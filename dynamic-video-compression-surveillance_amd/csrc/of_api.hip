@@ -510,16 +510,12 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         if ((e = of_alloc(h, a.ptr, a.bytes)) != hipSuccess) return bad(e, "hipMalloc");
     if (p.flags & DVC_FLAG_KEEP_PLANES)
         if ((e = of_alloc(h, &b.dbg_flow, 8 * N)) != hipSuccess) return bad(e, "hipMalloc");
-    if (g.sliding) {   // k_flow_scan hand-off state, sized for the largest level
-        size_t cells = 0, strips = 0;
-        for (int k = 0; k <= L; ++k) {
-            const size_t sk = dvc::of_scan_strips(h->lv[k].w);
-            cells = std::max(cells, sk * h->lv[k].h);
-            strips = std::max(strips, sk);
-        }
-        if ((e = of_alloc(h, &b.scan_g, 8 * 5 * cells * mb)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = of_alloc(h, &b.scan_flags, 8 * strips * mb)) != hipSuccess) return bad(e, "hipMalloc");
-        if ((e = hipMemset(b.scan_flags, 0, 8 * strips * mb)) != hipSuccess) return bad(e, "hipMemset");
+    if (g.sliding) {   // k_flow_scan hand-off slots, sized for the largest level
+        size_t slots = 0;
+        for (int k = 0; k <= L; ++k) slots = std::max(slots, dvc::of_scan_slots(g, h->lv[k].w, h->lv[k].h));
+        // tags start at 0, below every launch's epoch (>= 1): no slot reads as published
+        if ((e = of_alloc(h, &b.scan_g, 16 * slots * mb)) != hipSuccess) return bad(e, "hipMalloc");
+        if ((e = hipMemset(b.scan_g, 0, 16 * slots * mb)) != hipSuccess) return bad(e, "hipMemset");
     }
     if ((e = hipMemset(b.scan_abort, 0, 4)) != hipSuccess) return bad(e, "hipMemset");
     uint8_t vt[256];

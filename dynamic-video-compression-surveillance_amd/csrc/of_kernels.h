@@ -93,9 +93,11 @@ struct OfBufs {
     uint32_t* nroots;      // n
     float* dbg_flow;       // nullable: final flow of the batch's last frame (W*H*2)
     unsigned long long* stats;  // 64 slots x 4: frames, motion px, components, static blocks
-    // k_flow_scan (sliding box sums): strip hand-off state
-    double* scan_g;                // n x strips x h x 5 running sums (sized for the largest level)
-    unsigned long long* scan_flags;   // n x strips
+    // k_flow_scan (sliding box sums): strip hand-off state, one 16-B slot per
+    // (frame, strip, row block, row, channel) — {tag, sum lo, sum hi, tag},
+    // 64 slots (1 KB, whole 128-B lines) per row block; sized for the largest
+    // level by of_scan_slots
+    uint32_t* scan_g;
     unsigned int* scan_ctr;        // work-item counters (SCAN_Q = 8 queues)
     unsigned int* scan_abort;      // a hand-off wait timed out
 };
@@ -129,8 +131,8 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
                           hipStream_t s, unsigned int* epoch);
-// strips of the sliding-sum kernel across a level of width w (at most: strips of 32 columns)
-inline int of_scan_strips(int w) { return (w + 31) / 32; }
+// hand-off slots (16 B each) k_flow_scan needs per frame at a level of w x h
+size_t of_scan_slots(const OfGeom& g, int w, int h);
 // vote (frames in order) -> close/open -> 8-CC bounding boxes -> rectangle mask
 hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s);
 // compress_with_motion (of:151-183) + the mask bytes

@@ -663,11 +663,11 @@ __global__ void __launch_bounds__(256) k_flow(FlowArgs A)
 struct ScanArgs {
     FlowArgs f;
     int S;                       // strips across the level
-    double* gpub;                // n x S x h x 5: state after each strip's last column, per row
-    unsigned long long* flags;   // n x S: (epoch << 32) | row blocks published
+    int NB;                      // row blocks down the level
+    uint32_t* gpub;              // n x S x NB x 64 slots of 16 B: {tag, lo, hi, tag} per (row, channel)
     unsigned int* next;          // SCAN_Q work-item counters, zeroed before the launch
     unsigned int* abort;         // a wait timed out (never in a correct run)
-    unsigned int epoch;          // launch number (flags of older launches compare lower)
+    unsigned int epoch;          // launch number >= 1: the tag of this launch's published slots
 };
 
 constexpr int SCAN_Q = 8;   // work queues (XCD groups of workgroups)
@@ -790,16 +790,32 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
     }
 }
 
-// Hand-offs between strips use agent-scope relaxed atomics for payload and
-// flag (sc1: coherent across XCDs without cache maintenance) — no agent-scope
-// fence: an acquire would invalidate the XCD's L2 under every other workgroup
-// and a release would write it back (measured: 20 us per row block with them).
-// The producer orders payload before flag by draining its stores (vmcnt(0));
-// the consumer's payload loads are issued after the flag load returned.
-__device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long long* flag, unsigned long long want)
+// Hand-off between strips: per (frame, strip, row block) the state of every
+// (row, channel) chain after the strip's last column, as one 16-byte slot
+// {epoch, double lo, double hi, epoch} written by one buffer_store_dwordx4 sc1
+// (write-through past the XCD's L2) and read by buffer_load_dwordx4 sc1 (past
+// L1) polls until both tags equal the launch's epoch. A slot is its own flag:
+// no separate flag store, no drain of the payload stores before it, one
+// round trip for the consumer instead of flag + payload. 16-B sc1 stores are
+// observed untorn on gfx950 (MI355X_MICROARCH.md, hand-off section: not an
+// architectural guarantee) and the two tags bracket the value, so a torn read
+// — a half from another launch — fails the tag test and is re-polled instead
+// of used. Every slot is written once per launch and a row block's 60 slots
+// fill whole 128-B lines of their own. A poll that ever exceeds ~1 s sets
+// `abort` (reported by the host as an error) instead of hanging.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int SCAN_RSRC_W3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
+constexpr int CPOL_SC1 = 16;               // gfx940+ cache policy bit: sc1
+
+__device__ __forceinline__ bool scan_poll(const ScanArgs& S, __amdgpu_buffer_rsrc_t r, uint32_t off, double& v)
 {
     unsigned spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    for (;;) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL_SC1);
+        if (q.x == S.epoch && q.w == S.epoch) {
+            v = __builtin_bit_cast(double, (unsigned long long)q.y | ((unsigned long long)q.z << 32));
+            return true;
+        }
         if (__hip_atomic_load(S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 24)) {      // ~1 s: never in a correct run
@@ -807,15 +823,16 @@ __device__ __forceinline__ bool scan_wait(const ScanArgs& S, const unsigned long
             return false;
         }
     }
-    asm volatile("" ::: "memory");
-    return true;
 }
 
 // SMODE: 0 zero flow, 2 a flow buffer; MM: the largest box radius m served
 // (sizes the per-thread M positions)
 #ifdef DVC_SCAN_STAMPS
 __device__ unsigned long long g_scan_stamps[32 * 96 * 8];
-#define STAMP(k) do { if (tid == 0 && t == 0 && w == A.g.W && s < 32 && yb < 96) \
+#ifndef DVC_SCAN_STAMP_TID
+#define DVC_SCAN_STAMP_TID 0   // the thread whose timeline is stamped (64: wave 1, an M wave)
+#endif
+#define STAMP(k) do { if (tid == DVC_SCAN_STAMP_TID && t == 0 && w == A.g.W && s < 32 && yb < 96) \
     g_scan_stamps[(s * 96 + yb) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP(k) do {} while (0)
@@ -836,15 +853,15 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
     const float* src = SMODE == 2 ? A.src + (size_t)t * lvpx * 2 : nullptr;
     float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
-    unsigned long long* myflag = S.flags + (size_t)t * S.S + s;
-    const unsigned long long* lflag = s > 0 ? myflag - 1 : nullptr;
-    double* gp_mine = S.gpub + ((size_t)t * S.S + s) * (size_t)h * 5;
-    const double* gp_left = s > 0 ? gp_mine - (size_t)h * 5 : nullptr;
-    const unsigned long long ep = (unsigned long long)S.epoch << 32;
+    // hand-off slots of (frame t, strip s): row block yb at + yb * 1 KB
+    const uint32_t slot_bytes = (uint32_t)S.NB * 64u * 16u;
+    uint32_t* gp_base = S.gpub + (size_t)(t * S.S + s) * (slot_bytes / 4);
+    const __amdgpu_buffer_rsrc_t r_mine =
+        __builtin_amdgcn_make_buffer_rsrc(gp_base, 0, (int)slot_bytes, SCAN_RSRC_W3);
+    const __amdgpu_buffer_rsrc_t r_left =
+        __builtin_amdgcn_make_buffer_rsrc(s > 0 ? gp_base - slot_bytes / 4 : gp_base, 0, (int)slot_bytes, SCAN_RSRC_W3);
     // M positions of rows [rlo, rhi] x the strip's NC columns, ring offsets;
-    // the pipelined blocks' M is done by waves 1.. only (NP threads): wave 0
-    // runs the horizontal chains and the hand-off, whose loads and drain must
-    // not queue behind prefetches (vmcnt is in order)
+    // the pipelined blocks' M is done by waves 1.. only (NP threads)
     constexpr int NP = NT - 64;
     constexpr int MQ = (RB * scan_nc(SW, MM) + NP - 1) / NP;
     auto place = [&](MatPos<MQ>& P, int q0, int rlo, int npos, int stride) {
@@ -866,13 +883,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         const int rhi = min(y0 + RB - 1 + m, h - 1);
         npos = rhi >= rlo ? (rhi - rlo + 1) * NC : 0;
     };
-    // vertical chains of this thread: (column, channel) ch = tid + NT k
-    const int nch = NC * 5;
-    constexpr int KV = (scan_nc(SW, MM) * 5 + NT - 1) / NT;
-    double vsum[KV];
-#pragma unroll
-    for (int k = 0; k < KV; ++k) vsum[k] = 0.0;
-    {   // 1. M of the first block, unpipelined
+    {   // 1. M of the first block, unpipelined (all threads)
         int rlo, npos;
         block_rows(0, rlo, npos);
         for (int q0 = tid; q0 < npos; q0 += NT * MQ) {
@@ -884,19 +895,115 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         }
         __syncthreads();
     }
-    // The pipelined blocks' M positions: P = block b+1 (its R loads in flight
-    // from the start of block b's step, its M written in b's phase 3), Q = block
-    // b+2 (its flow loads in flight across b's step). Every thread issues its
-    // loads unconditionally from valid, clamped positions (wave 0 and positions
+    // Per row block b, three phases separated by the workgroup's barriers, with
+    // the roles split by wave (two loops, one per role, the same barriers):
+    //   wave 0 (the hand-off wave): phase 1 polls the left strip's flag for b
+    //     and loads its published state; phase 2 runs the horizontal chains of
+    //     b and stores their final state (sc1) for the right strip; phase 3
+    //     drains those stores and raises its own flag. Wave 0 issues no other
+    //     vector-memory instruction, so no wait of its own queues behind a
+    //     prefetch or a flow store (vmcnt is in order).
+    //   waves 1.. (M waves): phase 1 issues block b+1's R loads and block b+2's
+    //     flow loads, then the vertical recurrences of b; phase 2 writes block
+    //     b+1's M into the ring (FarnebackUpdateMatrices); phase 3 solves b.
+    const int slot_last = (h - 1) % RING;
+    if (tid < 64) {
+        for (int y0 = 0; y0 < h; y0 += RB) {
+            const int yb = y0 / RB, nrow = min(RB, h - y0);
+            STAMP(0);
+            // phase 1: the left strip's state after its last column, lanes
+            // (row i, channel c) of block b: poll the slot until published
+            double acc = 0.0;
+            if (s > 0 && tid < nrow * 5 && !scan_poll(S, r_left, (uint32_t)(yb * 64 + tid) * 16u, acc))
+                *s_alive = 0;
+            STAMP(2);
+            STAMP(7);
+            __syncthreads();   // A: the block's vertical sums are in sV
+            STAMP(1);
+            // phase 2: the horizontal recurrence, lanes (row i, channel c):
+            // g += vsum[x+m] - vsum[x-m-1], from the left strip's state (strip 0:
+            // OpenCV's (m+2) vsum[0] + vsum[1..m-1] start); g[x] overwrites the
+            // consumed vsum[x-m-1] (column x - X0 of sV)
+            if (tid < nrow * 5) {
+                const int i = tid / 5, c = tid - 5 * i;
+                double* v = sV + i * VS + c;   // column j at v[5 j]
+                if (s == 0) {
+                    acc = v[(0 - CX0) * 5] * (double)(m + 2);
+                    for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
+                }
+                const int ahead = 2 * m + 1;   // column of vsum[x+m] relative to vsum[x-m-1]
+                constexpr int U = 8;
+                int xl = 0;
+                // software-pipelined: the next U steps' LDS loads are in flight
+                // while this U steps' adds run (they read columns >= xl + U,
+                // which this U steps' stores to columns xl .. xl+U-1 never touch)
+                double da[U], db[U];
+                if (nx >= U) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        da[u] = v[(u + ahead) * 5];
+                        db[u] = v[u * 5];
+                    }
+                }
+                for (; xl + U <= nx; xl += U) {
+                    double na[U], nb[U];
+                    const bool more = xl + 2 * U <= nx;
+                    if (more) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            na[u] = v[(xl + U + u + ahead) * 5];
+                            nb[u] = v[(xl + U + u) * 5];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        acc += da[u] - db[u];
+                        v[(xl + u) * 5] = acc;
+                    }
+                    if (more) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            da[u] = na[u];
+                            db[u] = nb[u];
+                        }
+                    }
+                }
+                for (; xl < nx; ++xl) {
+                    const double d = v[(xl + ahead) * 5] - v[xl * 5];
+                    acc += d;
+                    v[xl * 5] = acc;
+                }
+                if (s + 1 < S.S) {   // the state after the strip's last column, for the right strip
+                    const unsigned long long bits = __builtin_bit_cast(unsigned long long, acc);
+                    const u32x4 q = {S.epoch, (uint32_t)bits, (uint32_t)(bits >> 32), S.epoch};
+                    __builtin_amdgcn_raw_buffer_store_b128(q, r_mine, (uint32_t)(yb * 64 + tid) * 16u, 0, CPOL_SC1);
+                }
+            }
+            STAMP(3);
+            __syncthreads();   // B
+            STAMP(4);
+            const bool alive = *s_alive;   // uniform: written before barrier A
+            // phase 3: nothing for wave 0 (the M waves solve the block)
+            __syncthreads();   // C: the next block's vertical sums overwrite sV
+            STAMP(5);
+            if (!alive) break;   // an aborted launch drains
+        }
+        return;
+    }
+    // M waves. The pipelined blocks' M positions: P = block b+1 (its R loads in
+    // flight from the start of block b's step, its M written in b's phase 2),
+    // Q = block b+2 (its flow loads in flight across b's step). Every thread
+    // issues its loads unconditionally from valid, clamped positions (positions
     // past the block are !ok and never stored): a load under a divergent branch
     // makes hipcc wait for it at the join, which would expose both global
     // latencies in every step.
+    const int mt = tid - 64;   // 0 .. NP-1
     int prow[MQ], pcol[MQ], pidx[MQ];   // this thread's pipelined positions: row in block, column
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
-        pidx[u] = tid - 64 + NP * u;
-        prow[u] = max(pidx[u], 0) / NC;
-        pcol[u] = max(pidx[u], 0) - prow[u] * NC;
+        pidx[u] = mt + NP * u;
+        prow[u] = pidx[u] / NC;
+        pcol[u] = pidx[u] - prow[u] * NC;
     }
     auto set_block = [&](MatPos<MQ>& Q, int yn) {   // positions of the block at row yn + stage 1
         int nlo, nnpos;
@@ -904,27 +1011,34 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         const int slo = nlo % RING;
 #pragma unroll
         for (int u = 0; u < MQ; ++u) {
-            Q.ok[u] = tid >= 64 && pidx[u] < nnpos;   // nnpos <= RB * NC <= NP * MQ
+            Q.ok[u] = pidx[u] < nnpos;   // nnpos <= RB * NC <= NP * MQ
             const int r = Q.ok[u] ? nlo + prow[u] : min(nlo, h - 1), sl = slo + (Q.ok[u] ? prow[u] : 0);
-            Q.xs[u] = min(max(CX0 + pcol[u], 0), w - 1);
+            Q.xs[u] = min(max(CX0 + (Q.ok[u] ? pcol[u] : 0), 0), w - 1);
             Q.ys[u] = r;
             Q.off[u] = ((sl >= RING ? sl - RING : sl) * NC + pcol[u]) * 5;
         }
         mat_stage1<MQ, SMODE>(A, src, Q);
     };
+    // vertical chains of this thread: (column, channel) ch = mt + NP k
+    const int nch = NC * 5;
+    constexpr int KV = (scan_nc(SW, MM) * 5 + NP - 1) / NP;
+    double vsum[KV];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) vsum[k] = 0.0;
     MatPos<MQ> P, Q;
     set_block(P, RB);
-    const int slot_last = (h - 1) % RING;
     for (int y0 = 0; y0 < h; y0 += RB) {
-        const int yb = y0 / RB, nrow = min(RB, h - y0);
+        const int nrow = min(RB, h - y0);
+        const int yb = y0 / RB;
+        (void)yb;
         STAMP(0);
         mat_stage2<MQ>(A, R0, R1, P);   // 1'. block b+1: R0 and the displaced R1 loads
         set_block(Q, y0 + 2 * RB);      //     block b+2: positions and flow loads
         STAMP(6);
-        // 2. vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
+        // phase 1: vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ch = tid + NT * k;
+            const int ch = mt + NP * k;
             if (ch >= nch) continue;
             const int j = ch / 5, c = ch - 5 * j;
             if (y0 == 0) {   // vsum = row0 * (m+2) (a float product) + rows 1..m-1
@@ -933,24 +1047,6 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             }
             // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0), stepped
             int sa = (y0 + m) % RING, sb = y0 - m - 1 >= 0 ? (y0 - m - 1) % RING : 0;
-            if (nrow == RB && y0 - m - 1 >= 0 && y0 + RB - 1 + m <= h - 1) {
-                // a block with no clamped row: all 2 RB ring loads issued before
-                // the first add of the chain (one LDS round trip, not RB)
-                float va[RB], vb[RB];
-#pragma unroll
-                for (int i = 0; i < RB; ++i) {
-                    const int ta = sa + i < RING ? sa + i : sa + i - RING;
-                    const int tb = sb + i < RING ? sb + i : sb + i - RING;
-                    va[i] = sM[(ta * NC + j) * 5 + c];
-                    vb[i] = sM[(tb * NC + j) * 5 + c];
-                }
-#pragma unroll
-                for (int i = 0; i < RB; ++i) {
-                    vsum[k] += (double)(va[i] - vb[i]);
-                    sV[i * VS + ch] = vsum[k];
-                }
-                continue;
-            }
             for (int i = 0; i < nrow; ++i) {
                 const int y = y0 + i;
                 const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
@@ -962,70 +1058,17 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             }
         }
         STAMP(7);
-        __syncthreads();   // the M ring is free from here: no reader until the next block's step 2
+        __syncthreads();   // A: the M ring is free from here: no reader until the next block's phase 1
         STAMP(1);
-        if (tid < 64) {
-            // 3. wave 0: the horizontal recurrence, lanes (row i, channel c):
-            // g += vsum[x+m] - vsum[x-m-1], from the left strip's published
-            // state (strip 0: OpenCV's (m+2) vsum[0] + vsum[1..m-1] start);
-            // g[x] overwrites the consumed vsum[x-m-1] (column x - X0 of sV).
-            // The state after the last column goes to the right neighbour:
-            // payload, drain (vmcnt: one wave), flag.
-            if (s > 0 && tid == 0) *s_alive = scan_wait(S, lflag, ep | (unsigned long long)(yb + 1)) ? 1 : 0;
-            STAMP(2);
-            if (tid < nrow * 5) {
-                const int i = tid / 5, c = tid - 5 * i;
-                double* v = sV + i * VS + c;   // column j at v[5 j]
-                double acc;
-                if (s == 0) {
-                    acc = v[(0 - CX0) * 5] * (double)(m + 2);
-                    for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
-                } else {
-                    acc = __hip_atomic_load(gp_left + (size_t)(y0 + i) * 5 + c, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const int ahead = 2 * m + 1;   // column of vsum[x+m] relative to vsum[x-m-1]
-                constexpr int U = 8;
-                int xl = 0;
-                for (; xl + U <= nx; xl += U) {   // all loads of 8 steps before their adds
-                    double da[U], db[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        da[u] = v[(xl + u + ahead) * 5];
-                        db[u] = v[(xl + u) * 5];
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        acc += da[u] - db[u];
-                        v[(xl + u) * 5] = acc;
-                    }
-                }
-                for (; xl < nx; ++xl) {
-                    const double d = v[(xl + ahead) * 5] - v[xl * 5];
-                    acc += d;
-                    v[xl * 5] = acc;
-                }
-                if (s + 1 < S.S)
-                    __hip_atomic_store(gp_mine + (size_t)(y0 + i) * 5 + c, acc, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (s + 1 < S.S) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's payload stores have landed
-                if (tid == 0)
-                    __hip_atomic_store(myflag, ep | (unsigned long long)(yb + 1), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else {
-            // 1''. waves 1..: the next block's M into the ring (its loads were
-            // issued at the start of the step), alongside wave 0's chains
-            mat_stage3<MQ>(A, P, sM);
-        }
+        // phase 2: the next block's M into the ring (its loads were issued at
+        // the start of the step), alongside wave 0's chains
+        mat_stage3<MQ>(A, P, sM);
         STAMP(3);
-        __syncthreads();
+        __syncthreads();   // B: the block's horizontal sums are in sV
         STAMP(4);
-        const bool alive = *s_alive;   // uniform: written before the previous barrier
-        // 4. flow = G^-1 h per pixel of the block (a wave = one row of 64 columns)
-        for (int e = tid; e < RB * SW; e += NT) {
+        const bool alive = *s_alive;   // uniform: written before barrier A
+        // phase 3: flow = G^-1 h per pixel of the block (a wave = one row of 64 columns)
+        for (int e = mt; e < RB * SW; e += NP) {
             const int i = e / SW, xl = e - i * SW;
             const int y = y0 + i, x = X0 + xl;
             const bool act = i < nrow && xl < nx;
@@ -1049,7 +1092,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fxo, fyo);
             }
         }
-        __syncthreads();   // the next block's step 2 overwrites sV
+        __syncthreads();   // C: the next block's phase 1 overwrites sV
         STAMP(5);
 #pragma unroll
         for (int u = 0; u < MQ; ++u) {   // block b+2 becomes the next step's b+1
@@ -1693,6 +1736,30 @@ __global__ void __launch_bounds__(256) k_flow_up(FlowArgs A, float* __restrict__
     }
 }
 
+// k_flow_scan variants for box radius m <= 4 (winsize <= 9, the reference's):
+// strips of 64 columns x blocks of RB rows, NT threads (the table below, the
+// launch switch in of_launch_flow); DVC_OF_SCAN=<index> picks one for A/B runs
+namespace {
+struct ScanCfg { int nt, rb; };
+constexpr ScanCfg kScanCfg4[] = {{512, 12}, {512, 6}, {256, 6}, {384, 6}, {256, 8}, {512, 8}};
+int scan_cfg_index()
+{
+    static const int v = [] {
+        const char* e = getenv("DVC_OF_SCAN");
+        const int k = e ? atoi(e) : 0;
+        return k >= 0 && k < (int)(sizeof(kScanCfg4) / sizeof(kScanCfg4[0])) ? k : 0;
+    }();
+    return v;
+}
+int scan_rb(const OfGeom& g) { return g.m <= 4 ? kScanCfg4[scan_cfg_index()].rb : 8; }
+}  // namespace
+
+size_t of_scan_slots(const OfGeom& g, int w, int h)
+{
+    const int rb = scan_rb(g);
+    return (size_t)((w + 63) / 64) * (size_t)((h + rb - 1) / rb) * 64;
+}
+
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
                           hipStream_t s, unsigned int* epoch)
 {
@@ -1730,22 +1797,13 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
             A.mring = b.mring;
             A.dbg_flow = b.dbg_flow;
             if (g.sliding) {   // OpenCV's running box sums: strip wavefront
-                // strips of 64 columns x blocks of RB rows, NT threads, OCC waves per
-                // SIMD (register budget); DVC_OF_SCAN=<index> picks a variant of the
-                // box radius m <= 4 table (winsize <= 9, the reference's) for A/B runs
-                struct Cfg { int nt, rb; };
-                static const Cfg cfg4[] = {{512, 12}, {512, 6}, {256, 6}, {384, 6}, {256, 8}, {512, 8}};
-                static const int scan_cfg = [] {
-                    const char* e = getenv("DVC_OF_SCAN");
-                    const int v = e ? atoi(e) : 0;
-                    return v >= 0 && v < 6 ? v : 0;
-                }();
-                const int sw = 64, rb = g.m <= 4 ? cfg4[scan_cfg].rb : 8;
+                const int scan_cfg = scan_cfg_index();
+                const int sw = 64, rb = scan_rb(g);
                 ScanArgs S{};
                 S.f = A;
                 S.S = (L.w + sw - 1) / sw;
+                S.NB = (L.h + rb - 1) / rb;
                 S.gpub = b.scan_g;
-                S.flags = b.scan_flags;
                 S.next = b.scan_ctr;
                 S.abort = b.scan_abort;
                 S.epoch = ++*epoch;
