@@ -145,12 +145,13 @@ def copy_bandwidth(local: int, nbytes=2 << 30, reps=20):
     """This GPU's streaming-copy rate in GB/s (bytes read + written), the
     practical ceiling SURVEY.md §8d asks the roofline to be quoted against
     beside the 8 TB/s spec: dvc_copy_rate, a hand-written 16-B-per-lane copy
-    (the form MI355X_MICROARCH.md measures 6.29 TB/s with) of a 2 GiB buffer,
-    with plain and with nontemporal stores; the faster of the two."""
+    (the form MI355X_MICROARCH.md measures 6.29 TB/s with; tools/copy_sweep.hip
+    picked its grid and unroll) of a 2 GiB buffer, with plain and with
+    nontemporal loads and stores; the faster of the two."""
     import dvc_amd
     plain = dvc_amd._native.copy_rate(local, nbytes, reps, nontemporal=False)
     nt = dvc_amd._native.copy_rate(local, nbytes, reps, nontemporal=True)
-    return max(plain, nt), {"plain_stores": round(plain, 1), "nontemporal_stores": round(nt, 1)}
+    return max(plain, nt), {"plain": round(plain, 1), "nontemporal": round(nt, 1)}
 
 
 def main():

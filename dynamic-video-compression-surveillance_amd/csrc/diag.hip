@@ -3,9 +3,12 @@
 // dvc_copy_rate: this device's practical streaming ceiling, the denominator
 // SURVEY.md §8d asks the FD roofline to be quoted against beside the 8 TB/s
 // spec. A hand-written copy in the form MI355X_MICROARCH.md measures its
-// 6.29 TB/s with (16 B per lane, coalesced, unrolled grid-stride), optionally
-// with nontemporal stores (what FD's output stages use), over a buffer far
-// beyond the 256 MB Infinity Cache; bytes read + written / event time.
+// 6.29 TB/s with (16 B per lane, coalesced, 4 vectors per lane in flight, one
+// workgroup per 16 KiB: tools/copy_sweep.hip measured it the fastest of the
+// unroll x grid x cache-policy forms on this pool's MI355X, 5.5-5.7 TB/s),
+// optionally with nontemporal loads and stores (what FD's streaming stages
+// use), over a buffer far beyond the 256 MB Infinity Cache; bytes read +
+// written / event time.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,6 +23,8 @@ namespace {
 constexpr int COPY_U = 4;   // 16-B vectors per lane per iteration (all loads before the stores)
 typedef float f4v __attribute__((ext_vector_type(4)));
 
+// one pass over the buffer (a workgroup per 256 x COPY_U 16-B vectors, no
+// grid stride): the fastest form of tools/copy_sweep.hip on MI355X
 template <bool NT>
 __global__ void __launch_bounds__(256) k_copy(const f4v* __restrict__ src, f4v* __restrict__ dst, size_t n4)
 {
@@ -29,7 +34,7 @@ __global__ void __launch_bounds__(256) k_copy(const f4v* __restrict__ src, f4v* 
 #pragma unroll
         for (int u = 0; u < COPY_U; ++u) {
             const size_t i = base + (size_t)u * 256;
-            if (i < n4) v[u] = src[i];
+            if (i < n4) v[u] = NT ? __builtin_nontemporal_load(src + i) : src[i];
         }
 #pragma unroll
         for (int u = 0; u < COPY_U; ++u) {
@@ -65,7 +70,8 @@ int dvc_copy_rate(int device, size_t bytes, int reps, int nontemporal, double* g
     float ms = 0.f;
     if (e == hipSuccess) {
         const size_t per_wg = (size_t)256 * COPY_U;
-        const unsigned grid = (unsigned)std::min<size_t>((n4 + per_wg - 1) / per_wg, (size_t)cus * 16);
+        const unsigned grid = (unsigned)((n4 + per_wg - 1) / per_wg);
+        (void)cus;
         auto launch = [&]() {
             if (nontemporal) hipLaunchKernelGGL(k_copy<true>, dim3(grid), dim3(256), 0, s, a, b, n4);
             else hipLaunchKernelGGL(k_copy<false>, dim3(grid), dim3(256), 0, s, a, b, n4);

@@ -976,6 +976,10 @@ __device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, 
     }
 }
 
+#ifndef DVC_OUT_NTLOAD
+#define DVC_OUT_NTLOAD 0
+#endif
+
 // k_out tile: 64 blocks across (64*B px) x 4 block rows, one wave per block
 // row, one lane per full BxB block, of frame t of the batch. FMT != BGR: the
 // block's pixels from a 4:2:0 surface (B luma bytes per row, the chroma row of
@@ -992,8 +996,15 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
 #pragma unroll
         for (int i = 0; i < B; ++i) {
             const uint32_t* src = reinterpret_cast<const uint32_t*>(f + (size_t)(by + i) * a.pitch + 3 * bx);
+#if DVC_OUT_NTLOAD
+            // the frame's last use (k_front read it a batch earlier): nontemporal
+            // loads leave L2 / MALL to the lines other stages re-read
+#pragma unroll
+            for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = __builtin_nontemporal_load(src + d);
+#else
 #pragma unroll
             for (int d = 0; d < 3 * B / 4; ++d) px[i][d] = src[d];
+#endif
         }
     } else {
 #pragma unroll

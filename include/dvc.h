@@ -430,8 +430,8 @@ int dvc_gaussian_taps_q8(int n, double sigma, uint16_t* taps);
  * against beside the 8 TB/s spec (SURVEY.md §8d "fraction of measured
  * stream-copy bandwidth on the same box"). A hand-written 16-B-per-lane copy
  * of `bytes` (use >> 256 MB, the Infinity Cache) repeated `reps` times on
- * `device`, nontemporal stores if `nontemporal`; *gbps = bytes read + written
- * per second / 1e9. */
+ * `device`, nontemporal loads and stores if `nontemporal`; *gbps = bytes
+ * read + written per second / 1e9. */
 int dvc_copy_rate(int device, size_t bytes, int reps, int nontemporal, double* gbps);
 
 #ifdef __cplusplus
