@@ -837,6 +837,12 @@ __device__ unsigned long long g_scan_stamps[32 * 96 * 8];
 #else
 #define STAMP(k) do {} while (0)
 #endif
+#ifndef DVC_SCAN_UF
+#define DVC_SCAN_UF 8   // columns per register set of the horizontal chains
+#endif
+#ifndef DVC_SCAN_PRIO
+#define DVC_SCAN_PRIO 0
+#endif
 template <int SW, int RB, int NT, int SMODE, int MM>
 __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, int* s_alive)
 {
@@ -908,6 +914,9 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
     //     b+1's M into the ring (FarnebackUpdateMatrices); phase 3 solves b.
     const int slot_last = (h - 1) % RING;
     if (tid < 64) {
+        // wave 0 carries the strip's critical path (the wavefront hand-off and
+        // the serial chains): issue priority over the M waves sharing its SIMD
+        if (DVC_SCAN_PRIO) __builtin_amdgcn_s_setprio(DVC_SCAN_PRIO);
         for (int y0 = 0; y0 < h; y0 += RB) {
             const int yb = y0 / RB, nrow = min(RB, h - y0);
             STAMP(0);
@@ -932,44 +941,40 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     for (int x = 1; x < m; ++x) acc += v[(x - CX0) * 5];
                 }
                 const int ahead = 2 * m + 1;   // column of vsum[x+m] relative to vsum[x-m-1]
-                constexpr int U = 8;
-                int xl = 0;
-                // software-pipelined: the next U steps' LDS loads are in flight
-                // while this U steps' adds run (they read columns >= xl + U,
-                // which this U steps' stores to columns xl .. xl+U-1 never touch)
-                double da[U], db[U];
-                if (nx >= U) {
+                // two register sets of UF columns in turn: set B's LDS loads are
+                // in flight while set A adds (they read columns >= x + UF, which
+                // A's stores to columns x .. x+UF-1 never touch), and no register
+                // copies between the sets, so the compiler's LDS waits count
+                // exactly the older loads
+                constexpr int UF = DVC_SCAN_UF;
+                const double* va = v + ahead * 5;
+                auto ld = [&](double (&da)[UF], double (&db)[UF], int x0) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        da[u] = v[(u + ahead) * 5];
-                        db[u] = v[u * 5];
+                    for (int u = 0; u < UF; ++u) {
+                        da[u] = va[(x0 + u) * 5];
+                        db[u] = v[(x0 + u) * 5];
                     }
-                }
-                for (; xl + U <= nx; xl += U) {
-                    double na[U], nb[U];
-                    const bool more = xl + 2 * U <= nx;
-                    if (more) {
+                };
+                auto add = [&](const double (&da)[UF], const double (&db)[UF], int x0) {
 #pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            na[u] = v[(xl + U + u + ahead) * 5];
-                            nb[u] = v[(xl + U + u) * 5];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
+                    for (int u = 0; u < UF; ++u) {
                         acc += da[u] - db[u];
-                        v[(xl + u) * 5] = acc;
+                        v[(x0 + u) * 5] = acc;
                     }
-                    if (more) {
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            da[u] = na[u];
-                            db[u] = nb[u];
-                        }
+                };
+                int xl = 0;
+                if (nx >= 2 * UF) {
+                    double a0[UF], b0[UF], a1[UF], b1[UF];
+                    ld(a0, b0, 0);
+                    for (; xl + 2 * UF <= nx; xl += 2 * UF) {
+                        ld(a1, b1, xl + UF);
+                        add(a0, b0, xl);
+                        if (xl + 3 * UF <= nx) ld(a0, b0, xl + 2 * UF);   // uniform
+                        add(a1, b1, xl + UF);
                     }
                 }
                 for (; xl < nx; ++xl) {
-                    const double d = v[(xl + ahead) * 5] - v[xl * 5];
+                    const double d = va[xl * 5] - v[xl * 5];
                     acc += d;
                     v[xl * 5] = acc;
                 }
@@ -988,6 +993,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
             STAMP(5);
             if (!alive) break;   // an aborted launch drains
         }
+        if (DVC_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
         return;
     }
     // M waves. The pipelined blocks' M positions: P = block b+1 (its R loads in
