@@ -28,7 +28,7 @@ def per_kernel(path, counter):
         if r.get("Counter_Name") != counter:
             continue
         name = r["Kernel_Name"]
-        key = name.split("(")[0].replace("void ", "").replace("dvc::", "").split("<")[0]
+        key = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("dvc::", "").split("<")[0]
         g = int(r.get("Grid_Size", 0) or 0)
         grid[key] = max(grid.get(key, 0), g)
         acc[(key, g)][int(r["Dispatch_Id"])] += float(r["Counter_Value"])

@@ -13,7 +13,7 @@ def main():
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         names = {}
         for r in csv.DictReader(open(path)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dvc::", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("dvc::", "")
             names[r["Dispatch_Id"]] = k
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         for d, cs in per.items():
