@@ -1710,35 +1710,44 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 // kernel computes inline per position (src_mode 1), same products, same order.
 // Four pixels per lane (two 16-B stores): the kernel writes 8 B/px and reads
 // the coarse flow from L2, so it is store-issue / HBM bound.
+constexpr int FU_ROWS = 4;   // rows per k_flow_up workgroup
 __global__ void __launch_bounds__(256) k_flow_up(FlowArgs A, float* __restrict__ out)
 {
+    // a workgroup = FU_ROWS rows of one frame (a few hundred thousand one-row
+    // workgroups cost more in dispatch than their loads and stores); a lane's
+    // column taps are loaded once for the rows
     const int w = A.lv.w, h = A.lv.h;
-    const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y, t = blockIdx.z;
-    if (x0 >= w || y >= h) return;
+    const int y0 = blockIdx.y * FU_ROWS, t = blockIdx.z;
     const float* src = A.src + (size_t)t * A.sw * A.sh * 2;
-    const LinTap ty = A.lv.uy[y];
-    const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
-    const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
-    float v[8];
+    for (int x0 = 4 * (int)threadIdx.x; x0 < w; x0 += 1024) {
+        LinTap tx[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const LinTap tx = A.lv.ux[min(x0 + k, w - 1)];
-        const float2 a0 = *reinterpret_cast<const float2*>(ra + tx.s0 * 2);
-        const float2 a1 = *reinterpret_cast<const float2*>(ra + tx.s1 * 2);
-        const float2 b0 = *reinterpret_cast<const float2*>(rb + tx.s0 * 2);
-        const float2 b1 = *reinterpret_cast<const float2*>(rb + tx.s1 * 2);
-        const float t0x = a0.x * tx.w0 + a1.x * tx.w1, t1x = b0.x * tx.w0 + b1.x * tx.w1;
-        const float t0y = a0.y * tx.w0 + a1.y * tx.w1, t1y = b0.y * tx.w0 + b1.y * tx.w1;
-        v[2 * k] = (t0x * ty.w0 + t1x * ty.w1) * A.g.up;
-        v[2 * k + 1] = (t0y * ty.w0 + t1y * ty.w1) * A.g.up;
-    }
-    float* o = out + ((size_t)t * w * h + (size_t)y * w + x0) * 2;
-    if (x0 + 4 <= w && !(w & 1)) {   // 16-B aligned: x0 % 4 == 0 and rows of an even width
-        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {   // the row's last lane, or rows of an odd width (8-B aligned only)
-        const int np = min(4, w - x0);
-        for (int k = 0; k < np; ++k) *reinterpret_cast<float2*>(o + 2 * k) = make_float2(v[2 * k], v[2 * k + 1]);
+        for (int k = 0; k < 4; ++k) tx[k] = A.lv.ux[min(x0 + k, w - 1)];
+        for (int y = y0; y < min(y0 + FU_ROWS, h); ++y) {
+            const LinTap ty = A.lv.uy[y];
+            const float* ra = src + (uint32_t)(ty.s0 * A.sw) * 2u;
+            const float* rb = src + (uint32_t)(ty.s1 * A.sw) * 2u;
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float2 a0 = *reinterpret_cast<const float2*>(ra + tx[k].s0 * 2);
+                const float2 a1 = *reinterpret_cast<const float2*>(ra + tx[k].s1 * 2);
+                const float2 b0 = *reinterpret_cast<const float2*>(rb + tx[k].s0 * 2);
+                const float2 b1 = *reinterpret_cast<const float2*>(rb + tx[k].s1 * 2);
+                const float t0x = a0.x * tx[k].w0 + a1.x * tx[k].w1, t1x = b0.x * tx[k].w0 + b1.x * tx[k].w1;
+                const float t0y = a0.y * tx[k].w0 + a1.y * tx[k].w1, t1y = b0.y * tx[k].w0 + b1.y * tx[k].w1;
+                v[2 * k] = (t0x * ty.w0 + t1x * ty.w1) * A.g.up;
+                v[2 * k + 1] = (t0y * ty.w0 + t1y * ty.w1) * A.g.up;
+            }
+            float* o = out + ((size_t)t * w * h + (size_t)y * w + x0) * 2;
+            if (x0 + 4 <= w && !(w & 1)) {   // 16-B aligned: x0 % 4 == 0 and rows of an even width
+                *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {   // the row's last lane, or rows of an odd width (8-B aligned only)
+                const int np = min(4, w - x0);
+                for (int k = 0; k < np; ++k) *reinterpret_cast<float2*>(o + 2 * k) = make_float2(v[2 * k], v[2 * k + 1]);
+            }
+        }
     }
 }
 
@@ -1816,7 +1825,7 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
                     // until iteration 1 writes it), then read it as a flow buffer
                     float* up = L.flow[1];
-                    hipLaunchKernelGGL(k_flow_up, dim3((L.w + 1023) / 1024, L.h, n), dim3(256), 0, s, A, up);
+                    hipLaunchKernelGGL(k_flow_up, dim3(1, (L.h + FU_ROWS - 1) / FU_ROWS, n), dim3(256), 0, s, A, up);
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
