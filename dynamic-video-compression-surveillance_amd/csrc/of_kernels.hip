@@ -258,51 +258,62 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 // ----------------------------------------------------------- level k > 0 ----
 // Horizontal smoothing pass (oc_blur_f32, first loop) of the full-resolution
 // gray at the 2w source columns the resize reads: tmpc[y][2dx] at xt[dx].s0,
-// tmpc[y][2dx+1] at xt[dx].s1. One workgroup per (row, frame), the gray row
-// staged in LDS (dynamic, GP bytes: whole dwords).
+// tmpc[y][2dx+1] at xt[dx].s1. One workgroup per PH_ROWS rows of a frame (a
+// workgroup per row spent more on dispatch than on its work), each row staged
+// in LDS (dynamic, 2 x GP bytes: whole dwords, double-buffered so row y+1's
+// loads fly while row y is blurred).
+constexpr int PH_ROWS = 4;
 __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
 {
     extern __shared__ uint32_t srow[];
-    const int y = blockIdx.x, t = blockIdx.y, W = g.W, H = g.H;
-    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(gray + (size_t)t * g.GP * H + (size_t)y * g.GP);
-    for (int i = threadIdx.x; i < g.GP / 4; i += 256) srow[i] = s32[i];
-    __syncthreads();
-    const uint8_t* s = reinterpret_cast<const uint8_t*>(srow);
-    const int r = lv.r, n2 = 2 * lv.w;
-    float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
-    for (int j = threadIdx.x; j < n2; j += 256) {
-        const LinTap tp = lv.xt[j >> 1];
-        const int c = (j & 1) ? tp.s1 : tp.s0;
-        float acc = lv.kf[r] * (float)s[c];
-        if (c >= r && c + r < W)   // taps inside the row: reflect101 is the identity
-            for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[c - i] + (float)s[c + i]);
-        else
-            for (int i = 1; i <= r; ++i)
-                acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
-        out[j] = acc;
+    const int t = blockIdx.y, W = g.W, H = g.H, y0 = blockIdx.x * PH_ROWS, ye = min(y0 + PH_ROWS, H);
+    const int nq = g.GP / 4, r = lv.r, n2 = 2 * lv.w;
+    const uint8_t* fr = gray + (size_t)t * g.GP * H;
+    for (int y = y0; y < ye; ++y) {
+        uint32_t* buf = srow + ((y - y0) & 1) * nq;
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(fr + (size_t)y * g.GP);
+        for (int i = threadIdx.x; i < nq; i += 256) buf[i] = s32[i];
+        __syncthreads();   // (also: the buffer's previous row, two rows back, is consumed)
+        const uint8_t* s = reinterpret_cast<const uint8_t*>(buf);
+        float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
+        for (int j = threadIdx.x; j < n2; j += 256) {
+            const LinTap tp = lv.xt[j >> 1];
+            const int c = (j & 1) ? tp.s1 : tp.s0;
+            float acc = lv.kf[r] * (float)s[c];
+            if (c >= r && c + r < W)   // taps inside the row: reflect101 is the identity
+                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[c - i] + (float)s[c + i]);
+            else
+                for (int i = 1; i <= r; ++i)
+                    acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
+            out[j] = acc;
+        }
     }
 }
 
 // Vertical smoothing pass (oc_blur_f32, second loop) at the 2h source rows the
 // resize reads: vtmp[2dy][j] at row yt[dy].s0, vtmp[2dy+1][j] at yt[dy].s1, for
-// every column slot j of tmpc — each blurred value the resize needs, once.
+// every column slot j of tmpc — each blurred value the resize needs, once. A
+// workgroup = 256 column slots x PV_ROWS output rows of a frame.
+constexpr int PV_ROWS = 8;
 __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
 {
-    const int j = blockIdx.x * 256 + threadIdx.x, yy = blockIdx.y, t = blockIdx.z;
-    const int H = g.H, n2 = 2 * lv.w, r = lv.r;
+    const int j = blockIdx.x * 256 + threadIdx.x, t = blockIdx.z;
+    const int H = g.H, n2 = 2 * lv.w, r = lv.r, yy0 = blockIdx.y * PV_ROWS, yye = min(yy0 + PV_ROWS, 2 * lv.h);
     if (j >= n2) return;
-    const LinTap ty = lv.yt[yy >> 1];
-    const int row = (yy & 1) ? ty.s1 : ty.s0;
     const float* T = lv.tmpc + (size_t)t * H * n2 + j;
-    float acc = lv.kf[r] * T[(size_t)row * n2];
-    if (row >= r && row + r < H) {   // uniform per workgroup (one row)
-        const float* C = T + (uint32_t)(row * n2);
-        for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (C[-(int)(i * n2)] + C[i * n2]);
-    } else {
-        for (int i = 1; i <= r; ++i)
-            acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
+    for (int yy = yy0; yy < yye; ++yy) {
+        const LinTap ty = lv.yt[yy >> 1];
+        const int row = (yy & 1) ? ty.s1 : ty.s0;
+        float acc = lv.kf[r] * T[(size_t)row * n2];
+        if (row >= r && row + r < H) {
+            const float* C = T + (uint32_t)(row * n2);
+            for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (C[-(int)(i * n2)] + C[i * n2]);
+        } else {
+            for (int i = 1; i <= r; ++i)
+                acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
+        }
+        lv.vtmp[((size_t)t * 2 * lv.h + yy) * n2 + j] = acc;
     }
-    lv.vtmp[((size_t)t * 2 * lv.h + yy) * n2 + j] = acc;
 }
 
 // The INTER_LINEAR combination (oc_resize_linear_f32) over tile + PN halo from
@@ -1074,19 +1085,32 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         STAMP(4);
         const bool alive = *s_alive;   // uniform: written before barrier A
         // phase 3: flow = G^-1 h per pixel of the block (a wave = one row of 64 columns)
-        for (int e = mt; e < RB * SW; e += NP) {
+        // a thread's pixels unrolled and branch-free (clamped LDS rows, results
+        // selected by `act`), so the scheduler interleaves their dependent
+        // chains (LDS loads, the f64 division); a wave's `act` lanes are its
+        // own, every wave runs the ballot of each of its pixels
+        constexpr int NQS = (RB * SW + NP - 1) / NP;
+        float fxs[NQS], fys[NQS];
+#pragma unroll
+        for (int q = 0; q < NQS; ++q) {
+            const int e = mt + NP * q;
+            const int i = e / SW, xl = e - i * SW;
+            const double* gg = sV + min(i, RB - 1) * VS + xl * 5;
+            const double g11 = gg[0] * g.box_scale, g12 = gg[1] * g.box_scale, g22 = gg[2] * g.box_scale;
+            const double h1 = gg[3] * g.box_scale, h2 = gg[4] * g.box_scale;
+            const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+            fxs[q] = (float)((g11 * h2 - g12 * h1) * idet);
+            fys[q] = (float)((g22 * h1 - g12 * h2) * idet);
+        }
+#pragma unroll
+        for (int q = 0; q < NQS; ++q) asm volatile("" ::"v"(fxs[q]), "v"(fys[q]));   // all solved before any store
+#pragma unroll
+        for (int q = 0; q < NQS; ++q) {
+            const int e = mt + NP * q;
             const int i = e / SW, xl = e - i * SW;
             const int y = y0 + i, x = X0 + xl;
             const bool act = i < nrow && xl < nx;
-            float fxo = 0.f, fyo = 0.f;
-            if (act) {
-                const double* gg = sV + i * VS + xl * 5;
-                const double g11 = gg[0] * g.box_scale, g12 = gg[1] * g.box_scale, g22 = gg[2] * g.box_scale;
-                const double h1 = gg[3] * g.box_scale, h2 = gg[4] * g.box_scale;
-                const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
-                fxo = (float)((g11 * h2 - g12 * h1) * idet);
-                fyo = (float)((g22 * h1 - g12 * h2) * idet);
-            }
+            const float fxo = act ? fxs[q] : 0.f, fyo = act ? fys[q] : 0.f;
             if (!A.last) {
                 if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fxo, fyo);
             } else {
@@ -1696,8 +1720,10 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 #undef DVC_FRONT0
     }
     for (int k = 1; k <= g.L; ++k) {
-        hipLaunchKernelGGL(k_pyr_h, dim3(g.H, n), dim3(256), (size_t)g.GP, s, g, lv[k], b.gray);
-        hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, 2 * lv[k].h, n), dim3(256), 0, s, g, lv[k]);
+        hipLaunchKernelGGL(k_pyr_h, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)2 * g.GP, s, g, lv[k],
+                           b.gray);
+        hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, (2 * lv[k].h + PV_ROWS - 1) / PV_ROWS, n), dim3(256),
+                           0, s, g, lv[k]);
         dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);
         if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, s, g, lv[k], a0);
         else hipLaunchKernelGGL(k_pyr_poly<7>, gp, dim3(256), 0, s, g, lv[k], a0);
