@@ -1546,6 +1546,18 @@ static int band_budget(const RowGeom& g)
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s)
 {
     if (!c.rowb) return hipErrorInvalidValue;   // every kernel below finds its nodes through rowb
+    // DVC_CCL_SUB=F (experiment): the five kernels over sub-batches of F frames
+    static const int sub = [] {
+        const char* e = getenv("DVC_CCL_SUB");
+        return e ? atoi(e) : 0;
+    }();
+    if (sub > 0 && n > sub) {
+        for (int f0 = 0; f0 < n; f0 += sub) {
+            const hipError_t e = launch_ccl(c.frame(f0, g), g, std::min(sub, n - f0), min_area2, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
     hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(256), band_lds(g, BH, budget), s, c, g, budget);
     if (nb > 1)

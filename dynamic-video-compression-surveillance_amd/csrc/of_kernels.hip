@@ -69,6 +69,9 @@ __device__ __forceinline__ float border_w(int d) { return d < 2 ? 0.14f : 0.4472
 namespace {
 
 constexpr int PT_W = 64, PT_H = 16;   // poly-expansion tile (level pixels)
+#ifndef DVC_POLY_FMA
+#define DVC_POLY_FMA 1
+#endif
 constexpr int FL_W = 32, FL_H = 16;   // flow tile (32 wide: <= 26 KB LDS, 6 workgroups per CU)
 
 // Ring slot of frame number a. The launchers pass frame numbers through
@@ -134,8 +137,16 @@ __device__ __forceinline__ void poly_tile(const float* sI, float* sv, const Poly
             const float* M = INT ? c - 3 * k : sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
             const float gk = pc.g[PN + k], xgk = pc.xg[PN + k];
             const double tg = (double)(P[0] + M[0]);
+#if DVC_POLY_FMA
+            // tg and the taps are floats: their double product has <= 48
+            // significant bits, so it is exact and fma(tg, g, b) rounds exactly
+            // as b + tg * g (one v_fma_f64 instead of v_mul_f64 + v_add_f64)
+            b1 = __builtin_fma(tg, (double)gk, b1);
+            b4 = __builtin_fma(tg, (double)pc.xxg[PN + k], b4);
+#else
             b1 += tg * (double)gk;
             b4 += tg * (double)pc.xxg[PN + k];
+#endif
             b2 += (double)((P[0] - M[0]) * xgk);
             b3 += (double)((P[1] + M[1]) * gk);
             b6 += (double)((P[1] - M[1]) * xgk);
@@ -689,7 +700,11 @@ constexpr int SCAN_Q = 8;   // work queues (XCD groups of workgroups)
 // the horizontal chains' lanes (row i, channel c) fall on distinct LDS bank
 // pairs, at most 2-way); the chains overwrite the consumed vertical sums with
 // the horizontal ones in place
-__host__ __device__ constexpr int scan_ring(int rb, int m) { return rb + 2 * m + 1; }
+// The M ring holds RB + 2m + 1 rows, rounded up to a multiple of RB: a block's
+// rows then start at one of RING / RB ring phases, and the vertical sums of an
+// interior block (m == the variant's MM) read their ring rows at compile-time
+// offsets of that phase (scan_vsum_rows) — no per-row slot arithmetic.
+__host__ __device__ constexpr int scan_ring(int rb, int m) { return (rb + 2 * m + 1 + rb - 1) / rb * rb; }
 __host__ __device__ constexpr int scan_nc(int sw, int m) { return sw + 2 * m + 1; }
 __host__ __device__ constexpr int scan_vs(int sw, int m) { return scan_nc(sw, m) * 5 + ((5 - scan_nc(sw, m) * 5) % 32 + 32) % 32; }
 inline size_t scan_lds_bytes(int sw, int rb, int m)
@@ -707,9 +722,23 @@ struct MatPos {
     int xs[MQ], ys[MQ], off[MQ];
     bool ok[MQ];
     float dx[MQ], dy[MQ], r0[MQ][5];   // stage 1
-    float fx[MQ], fy[MQ], pq[MQ][20];  // stage 2
-    bool inb[MQ];
+    float pq[MQ][20];                  // stage 2 (the bilinear fractions and the
+                                       // in-bounds test are recomputed in stage 3
+                                       // rather than held across the step)
 };
+
+// the displaced position (x + dx, y + dy) of FarnebackUpdateMatrices: its
+// integer corner and fractions, and whether the 2x2 neighbourhood is inside
+__device__ __forceinline__ bool mat_corner(int x, int y, float dx, float dy, int w, int h, int& x1, int& y1,
+                                           float& fx, float& fy)
+{
+    const float px = (float)x + dx, py = (float)y + dy;
+    x1 = (int)floorf(px);
+    y1 = (int)floorf(py);
+    fx = px - (float)x1;
+    fy = py - (float)y1;
+    return (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
+}
 
 // stage 1: the flow loads (src_mode 2; the scan kernel's source flow is never
 // the coarser level's: k_flow_up upsamples it to a flow buffer first)
@@ -738,11 +767,9 @@ __device__ __forceinline__ void mat_stage2(const FlowArgs& A, const float* __res
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
         ld5(R0 + 5u * (uint32_t)(P.ys[u] * w + P.xs[u]), P.r0[u]);   // (independent of the flow)
-        const float fx = (float)P.xs[u] + P.dx[u], fy = (float)P.ys[u] + P.dy[u];
-        const int x1 = (int)floorf(fx), y1 = (int)floorf(fy);
-        P.fx[u] = fx - (float)x1;
-        P.fy[u] = fy - (float)y1;
-        P.inb[u] = (unsigned)x1 < (unsigned)(w - 1) && (unsigned)y1 < (unsigned)(h - 1);
+        int x1, y1;
+        float fx, fy;
+        (void)mat_corner(P.xs[u], P.ys[u], P.dx[u], P.dy[u], w, h, x1, y1, fx, fy);
         const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
         const float* p = R1 + 5u * (uint32_t)(y1c * w + x1c);
         const float* q = p + 5u * (uint32_t)w;
@@ -759,14 +786,17 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
     for (int u = 0; u < MQ; ++u) {
         if (!P.ok[u]) continue;
         const int x = P.xs[u], y = P.ys[u];
-        const float dx = P.dx[u], dy = P.dy[u], fx = P.fx[u], fy = P.fy[u];
+        const float dx = P.dx[u], dy = P.dy[u];
+        int x1, y1;
+        float fx, fy;
+        const bool inb = mat_corner(x, y, dx, dy, w, h, x1, y1, fx, fy);
         const float* r0 = P.r0[u];
         const float* p = P.pq[u];
         const float* q = P.pq[u] + 10;
         f32x2 R23, R45;
         float r6;
         const f32x2 R0_01 = {r0[0], r0[1]}, R0_23 = {r0[2], r0[3]};
-        if (P.inb[u]) {
+        if (inb) {
             const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
             const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
             const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
@@ -854,6 +884,55 @@ __device__ unsigned long long g_scan_stamps[32 * 96 * 8];
 #ifndef DVC_SCAN_PRIO
 #define DVC_SCAN_PRIO 0
 #endif
+#ifndef DVC_SCAN_FG
+#define DVC_SCAN_FG 2   // rows per group of the fast vertical sums' ring loads
+#endif
+#ifndef DVC_SCAN_VG
+#define DVC_SCAN_VG 1   // rows per group of the generic vertical sums' ring loads
+#endif
+// Vertical running sums of one (column, channel) chain over an interior block
+// of RB rows whose first row sits at ring phase PH (y0 % RING == PH * RB), box
+// radius M: vsum += (double)(M[y+M] - M[y-M-1]) row by row, OpenCV's order.
+// Every ring and sV offset is a constant: per row two ds_read_b32 and one
+// ds_write_b64 with immediate offsets and the three VALU ops of the sum (the
+// generic loop spends ~30 instructions a row on slot arithmetic, and a wave
+// issues at most one instruction every ~4 cycles).
+template <int SW, int RB, int M, int PH>
+__device__ __forceinline__ void scan_vsum_rows(const float* mc, double* vc, double& v)
+{
+    constexpr int RING = scan_ring(RB, M), ROW = scan_nc(SW, M) * 5, VS = scan_vs(SW, M);
+    constexpr int G = DVC_SCAN_FG;   // rows whose loads are issued together
+#pragma unroll
+    for (int i0 = 0; i0 < RB; i0 += G) {
+        float fa[G], fb[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int i = i0 + u;
+            if (i < RB) {
+                fa[u] = mc[((PH * RB + M + i) % RING) * ROW];
+                fb[u] = mc[((PH * RB + RING - M - 1 + i) % RING) * ROW];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int i = i0 + u;
+            if (i < RB) {
+                v += (double)(fa[u] - fb[u]);
+                vc[i * VS] = v;
+            }
+        }
+    }
+}
+
+template <int SW, int RB, int M, int PH = 0>
+__device__ __forceinline__ void scan_vsum_phase(int ph, const float* mc, double* vc, double& v)
+{
+    if constexpr (PH < scan_ring(RB, M) / RB) {
+        if (ph == PH) scan_vsum_rows<SW, RB, M, PH>(mc, vc, v);
+        else scan_vsum_phase<SW, RB, M, PH + 1>(ph, mc, vc, v);
+    }
+}
+
 template <int SW, int RB, int NT, int SMODE, int MM>
 __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* sV, int* s_alive)
 {
@@ -1053,6 +1132,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         set_block(Q, y0 + 2 * RB);      //     block b+2: positions and flow loads
         STAMP(6);
         // phase 1: vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
+        const bool fast = m == MM && y0 - m - 1 >= 0 && y0 + RB - 1 + m <= h - 1;   // uniform
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ch = mt + NP * k;
@@ -1062,16 +1142,34 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                 vsum[k] = (double)(sM[j * 5 + c] * (float)(m + 2));
                 for (int r = 1; r < m; ++r) vsum[k] += (double)sM[((min(r, h - 1) % RING) * NC + j) * 5 + c];
             }
-            // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0), stepped
+            const float* mc = sM + j * 5 + c;
+            if (fast) {   // uniform: an interior block at the variant's radius
+                scan_vsum_phase<SW, RB, MM>((y0 % RING) / RB, mc, sV + ch, vsum[k]);
+                continue;
+            }
+            // ring slots of rows y+m (clamped to h-1) and y-m-1 (clamped to 0),
+            // stepped (uniform); rows in groups of VG, the group's ring loads
+            // issued together
             int sa = (y0 + m) % RING, sb = y0 - m - 1 >= 0 ? (y0 - m - 1) % RING : 0;
-            for (int i = 0; i < nrow; ++i) {
-                const int y = y0 + i;
-                const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
-                const float dd = sM[(ta * NC + j) * 5 + c] - sM[(tb * NC + j) * 5 + c];
-                vsum[k] += (double)dd;
-                sV[i * VS + ch] = vsum[k];
-                sa = sa + 1 == RING ? 0 : sa + 1;
-                if (y - m - 1 >= 0) sb = sb + 1 == RING ? 0 : sb + 1;
+            constexpr int VG = DVC_SCAN_VG;
+            for (int i0 = 0; i0 < nrow; i0 += VG) {
+                float fa[VG], fb[VG];
+#pragma unroll
+                for (int u = 0; u < VG; ++u) {   // rows past the block read valid (clamped) slots, unused
+                    const int y = y0 + i0 + u;
+                    const int ta = y + m <= h - 1 ? sa : slot_last, tb = y - m - 1 >= 0 ? sb : 0;
+                    fa[u] = mc[ta * NC * 5];
+                    fb[u] = mc[tb * NC * 5];
+                    sa = sa + 1 == RING ? 0 : sa + 1;
+                    if (y - m - 1 >= 0) sb = sb + 1 == RING ? 0 : sb + 1;
+                }
+#pragma unroll
+                for (int u = 0; u < VG; ++u) {
+                    if (i0 + u < nrow) {
+                        vsum[k] += (double)(fa[u] - fb[u]);
+                        sV[(i0 + u) * VS + ch] = vsum[k];
+                    }
+                }
             }
         }
         STAMP(7);
