@@ -759,13 +759,13 @@ __device__ __forceinline__ void mat_stage1(const FlowArgs& A, const float* src, 
     }
 }
 
-template <int MQ>
+template <int MQ, int U0 = 0, int U1 = MQ>
 __device__ __forceinline__ void mat_stage2(const FlowArgs& A, const float* __restrict__ R0,
                                            const float* __restrict__ R1, MatPos<MQ>& P)
 {
     const int w = A.lv.w, h = A.lv.h;
 #pragma unroll
-    for (int u = 0; u < MQ; ++u) {
+    for (int u = U0; u < U1; ++u) {
         ld5(R0 + 5u * (uint32_t)(P.ys[u] * w + P.xs[u]), P.r0[u]);   // (independent of the flow)
         int x1, y1;
         float fx, fy;
@@ -887,6 +887,9 @@ __device__ unsigned long long g_scan_stamps[32 * 96 * 8];
 #ifndef DVC_SCAN_FG
 #define DVC_SCAN_FG 2   // rows per group of the fast vertical sums' ring loads
 #endif
+#ifndef DVC_SCAN_ILV
+#define DVC_SCAN_ILV 1   // interleave the M gathers with the vertical sums (interior blocks)
+#endif
 #ifndef DVC_SCAN_VG
 #define DVC_SCAN_VG 1   // rows per group of the generic vertical sums' ring loads
 #endif
@@ -897,18 +900,18 @@ __device__ unsigned long long g_scan_stamps[32 * 96 * 8];
 // ds_write_b64 with immediate offsets and the three VALU ops of the sum (the
 // generic loop spends ~30 instructions a row on slot arithmetic, and a wave
 // issues at most one instruction every ~4 cycles).
-template <int SW, int RB, int M, int PH>
+template <int SW, int RB, int M, int PH, int I0 = 0, int I1 = RB>
 __device__ __forceinline__ void scan_vsum_rows(const float* mc, double* vc, double& v)
 {
     constexpr int RING = scan_ring(RB, M), ROW = scan_nc(SW, M) * 5, VS = scan_vs(SW, M);
     constexpr int G = DVC_SCAN_FG;   // rows whose loads are issued together
 #pragma unroll
-    for (int i0 = 0; i0 < RB; i0 += G) {
+    for (int i0 = I0; i0 < I1; i0 += G) {
         float fa[G], fb[G];
 #pragma unroll
         for (int u = 0; u < G; ++u) {
             const int i = i0 + u;
-            if (i < RB) {
+            if (i < I1) {
                 fa[u] = mc[((PH * RB + M + i) % RING) * ROW];
                 fb[u] = mc[((PH * RB + RING - M - 1 + i) % RING) * ROW];
             }
@@ -916,7 +919,7 @@ __device__ __forceinline__ void scan_vsum_rows(const float* mc, double* vc, doub
 #pragma unroll
         for (int u = 0; u < G; ++u) {
             const int i = i0 + u;
-            if (i < RB) {
+            if (i < I1) {
                 v += (double)(fa[u] - fb[u]);
                 vc[i * VS] = v;
             }
@@ -930,6 +933,36 @@ __device__ __forceinline__ void scan_vsum_phase(int ph, const float* mc, double*
     if constexpr (PH < scan_ring(RB, M) / RB) {
         if (ph == PH) scan_vsum_rows<SW, RB, M, PH>(mc, vc, v);
         else scan_vsum_phase<SW, RB, M, PH + 1>(ph, mc, vc, v);
+    }
+}
+
+// Phase 1 of an interior block for the M waves with one vertical chain each:
+// the gathers of block b+1 position by position, each followed by a slice of
+// the vertical sums, so the texture addresser drains one position's loads
+// while the wave runs the next rows' LDS and VALU work (a burst of every
+// gather at the start of the step queued ~0.9 us of vector-memory issue ahead
+// of the sums). The ring phase is dispatched per slice: the uniform branch
+// keeps each position's loads after the previous slice in program order.
+template <int SW, int RB, int M, int I0, int I1, int PH = 0>
+__device__ __forceinline__ void scan_vsum_slice(int ph, const float* mc, double* vc, double& v)
+{
+    if constexpr (PH < scan_ring(RB, M) / RB) {
+        if (ph == PH) scan_vsum_rows<SW, RB, M, PH, I0, I1>(mc, vc, v);
+        else scan_vsum_slice<SW, RB, M, I0, I1, PH + 1>(ph, mc, vc, v);
+    }
+}
+
+template <int SW, int RB, int M, int MQ, int U = 0>
+__device__ __forceinline__ void scan_phase1_ilv(int ph, const FlowArgs& A, const float* __restrict__ R0,
+                                                const float* __restrict__ R1, MatPos<MQ>& P, const float* mc,
+                                                double* vc, double& v)
+{
+    if constexpr (U < MQ) {
+        mat_stage2<MQ, U, U + 1>(A, R0, R1, P);
+        __builtin_amdgcn_sched_barrier(0);
+        scan_vsum_slice<SW, RB, M, RB * U / MQ, RB * (U + 1) / MQ>(ph, mc, vc, v);
+        __builtin_amdgcn_sched_barrier(0);
+        scan_phase1_ilv<SW, RB, M, MQ, U + 1>(ph, A, R0, R1, P, mc, vc, v);
     }
 }
 
@@ -1128,15 +1161,25 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
         const int yb = y0 / RB;
         (void)yb;
         STAMP(0);
+        // phase 1: vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
+        const bool fast = m == MM && y0 - m - 1 >= 0 && y0 + RB - 1 + m <= h - 1;   // uniform
+        if (KV == 1 && fast && DVC_SCAN_ILV) {
+            // every thread runs a chain (threads past the last one repeat it:
+            // same values to the same sV words), so the block is straight-line
+            const int chc = min(mt, nch - 1), jc = chc / 5, cc = chc - 5 * jc;
+            scan_phase1_ilv<SW, RB, MM, MQ>((y0 % RING) / RB, A, R0, R1, P, sM + jc * 5 + cc, sV + chc, vsum[0]);
+            set_block(Q, y0 + 2 * RB);   // block b+2: positions and flow loads
+            STAMP(6);
+        } else {
         mat_stage2<MQ>(A, R0, R1, P);   // 1'. block b+1: R0 and the displaced R1 loads
         set_block(Q, y0 + 2 * RB);      //     block b+2: positions and flow loads
         STAMP(6);
-        // phase 1: vertical recurrence for the block's rows: vsum += (float)(M[y+m] - M[y-m-1])
-        const bool fast = m == MM && y0 - m - 1 >= 0 && y0 + RB - 1 + m <= h - 1;   // uniform
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ch = mt + NP * k;
-            if (ch >= nch) continue;
+            // threads past the last chain repeat it (same values to the same sV
+            // words), so every thread's vsum is a valid chain state for the
+            // straight-line interleaved path above
+            const int ch = min(mt + NP * k, nch - 1);
             const int j = ch / 5, c = ch - 5 * j;
             if (y0 == 0) {   // vsum = row0 * (m+2) (a float product) + rows 1..m-1
                 vsum[k] = (double)(sM[j * 5 + c] * (float)(m + 2));
@@ -1171,6 +1214,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                     }
                 }
             }
+        }
         }
         STAMP(7);
         __syncthreads();   // A: the M ring is free from here: no reader until the next block's phase 1
