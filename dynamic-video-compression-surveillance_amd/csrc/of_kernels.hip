@@ -1878,7 +1878,60 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 // kernel computes inline per position (src_mode 1), same products, same order.
 // Four pixels per lane (two 16-B stores): the kernel writes 8 B/px and reads
 // the coarse flow from L2, so it is store-issue / HBM bound.
-constexpr int FU_ROWS = 4;   // rows per k_flow_up workgroup
+// LDS-staged form (lv.up_rows > 0): the workgroup's coarse rows are loaded
+// once as 16-B words and the four taps of every output pixel read from LDS —
+// the gather form spent four 8-B vector-memory loads per pixel, texture-
+// addresser bound (~4x the time of its 8-B/px stores). Same products, same
+// order, so the same bits.
+__global__ void __launch_bounds__(256) k_flow_up_lds(FlowArgs A, float* __restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 sup[];
+    const int w = A.lv.w, h = A.lv.h, sw = A.sw;
+    const int y0 = blockIdx.y * FU_ROWS, ye = min(y0 + FU_ROWS, h), t = blockIdx.z;
+    const float* src = A.src + (size_t)t * sw * A.sh * 2;
+    const int r0 = A.lv.uy[y0].s0, nr = A.lv.uy[ye - 1].s1 - r0 + 1;   // <= lv.up_rows (host)
+    {   // rows r0 .. r0+nr-1: contiguous floats r0*sw*2 ..
+        const float* s0p = src + (size_t)r0 * sw * 2;
+        const int nf = nr * sw * 2;
+        const bool al = (((uintptr_t)s0p) & 15u) == 0;
+        if (al) {
+            for (int i = threadIdx.x; 4 * i + 3 < nf; i += 256)
+                reinterpret_cast<float4*>(sup)[i] = reinterpret_cast<const float4*>(s0p)[i];
+            for (int i = (nf & ~3) + threadIdx.x; i < nf; i += 256) reinterpret_cast<float*>(sup)[i] = s0p[i];
+        } else {
+            for (int i = threadIdx.x; i < nf; i += 256) reinterpret_cast<float*>(sup)[i] = s0p[i];
+        }
+    }
+    __syncthreads();
+    for (int x0 = 4 * (int)threadIdx.x; x0 < w; x0 += 1024) {
+        LinTap tx[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tx[k] = A.lv.ux[min(x0 + k, w - 1)];
+        for (int y = y0; y < ye; ++y) {
+            const LinTap ty = A.lv.uy[y];
+            const float2* ra = sup + (ty.s0 - r0) * sw;
+            const float2* rb = sup + (ty.s1 - r0) * sw;
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float2 a0 = ra[tx[k].s0], a1 = ra[tx[k].s1], b0 = rb[tx[k].s0], b1 = rb[tx[k].s1];
+                const float t0x = a0.x * tx[k].w0 + a1.x * tx[k].w1, t1x = b0.x * tx[k].w0 + b1.x * tx[k].w1;
+                const float t0y = a0.y * tx[k].w0 + a1.y * tx[k].w1, t1y = b0.y * tx[k].w0 + b1.y * tx[k].w1;
+                v[2 * k] = (t0x * ty.w0 + t1x * ty.w1) * A.g.up;
+                v[2 * k + 1] = (t0y * ty.w0 + t1y * ty.w1) * A.g.up;
+            }
+            float* o = out + ((size_t)t * w * h + (size_t)y * w + x0) * 2;
+            if (x0 + 4 <= w && !(w & 1)) {
+                *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                const int np = min(4, w - x0);
+                for (int k = 0; k < np; ++k) *reinterpret_cast<float2*>(o + 2 * k) = make_float2(v[2 * k], v[2 * k + 1]);
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_flow_up(FlowArgs A, float* __restrict__ out)
 {
     // a workgroup = FU_ROWS rows of one frame (a few hundred thousand one-row
@@ -1993,7 +2046,11 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
                     // until iteration 1 writes it), then read it as a flow buffer
                     float* up = L.flow[1];
-                    hipLaunchKernelGGL(k_flow_up, dim3(1, (L.h + FU_ROWS - 1) / FU_ROWS, n), dim3(256), 0, s, A, up);
+                    const dim3 gu(1, (L.h + FU_ROWS - 1) / FU_ROWS, n);
+                    if (L.up_rows > 0 && !getenv("DVC_OF_UP_GATHER"))
+                        hipLaunchKernelGGL(k_flow_up_lds, gu, dim3(256), (size_t)L.up_rows * A.sw * 8, s, A, up);
+                    else
+                        hipLaunchKernelGGL(k_flow_up, gu, dim3(256), 0, s, A, up);
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
