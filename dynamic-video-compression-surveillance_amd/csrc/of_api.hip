@@ -424,8 +424,20 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     for (hipEvent_t* ev : {&h->ev_user, &h->ev_join})
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     h->s_pyr = h->stream;
-    for (hipStream_t* st : {&h->s_flow, &h->s_mask})
-        if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    {
+        // DVC_OF_PRIO=<flow><mask> (experiments): h / n / l stream priority each
+        const char* pe = getenv("DVC_OF_PRIO");
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        auto prio = [&](int i) {
+            const char c = pe && (int)strlen(pe) > i ? pe[i] : 'n';
+            return c == 'h' ? hi : (c == 'l' ? lo : 0);
+        };
+        hipStream_t* ss[2] = {&h->s_flow, &h->s_mask};
+        for (int i = 0; i < 2; ++i)
+            if ((e = hipStreamCreateWithPriority(ss[i], hipStreamNonBlocking, prio(i))) != hipSuccess)
+                return bad(e, "hipStreamCreate");
+    }
     for (OfSlot& sl : h->slot)
         for (hipEvent_t* ev : {&sl.ev_pyr, &sl.ev_flow, &sl.ev_mask})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");

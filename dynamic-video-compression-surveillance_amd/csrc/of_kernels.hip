@@ -274,28 +274,57 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 // in LDS (dynamic, 2 x GP bytes: whole dwords, double-buffered so row y+1's
 // loads fly while row y is blurred).
 constexpr int PH_ROWS = 4;
+constexpr int PH_J = 8;   // column slots per thread (n2 <= 256 * PH_J: the taps' columns kept in registers)
 __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
 {
-    extern __shared__ uint32_t srow[];
+    // the row as floats in LDS (each tap one ds_read_b32, no byte convert), the
+    // thread's source columns loaded once for the workgroup's rows
+    extern __shared__ float srowf[];
     const int t = blockIdx.y, W = g.W, H = g.H, y0 = blockIdx.x * PH_ROWS, ye = min(y0 + PH_ROWS, H);
     const int nq = g.GP / 4, r = lv.r, n2 = 2 * lv.w;
     const uint8_t* fr = gray + (size_t)t * g.GP * H;
-    for (int y = y0; y < ye; ++y) {
-        uint32_t* buf = srow + ((y - y0) & 1) * nq;
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(fr + (size_t)y * g.GP);
-        for (int i = threadIdx.x; i < nq; i += 256) buf[i] = s32[i];
-        __syncthreads();   // (also: the buffer's previous row, two rows back, is consumed)
-        const uint8_t* s = reinterpret_cast<const uint8_t*>(buf);
-        float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
-        for (int j = threadIdx.x; j < n2; j += 256) {
+    int col[PH_J];
+#pragma unroll
+    for (int q = 0; q < PH_J; ++q) {
+        const int j = threadIdx.x + 256 * q;
+        col[q] = 0;
+        if (j < n2) {
             const LinTap tp = lv.xt[j >> 1];
-            const int c = (j & 1) ? tp.s1 : tp.s0;
-            float acc = lv.kf[r] * (float)s[c];
+            col[q] = (j & 1) ? tp.s1 : tp.s0;
+        }
+    }
+    for (int y = y0; y < ye; ++y) {
+        float* buf = srowf + ((y - y0) & 1) * g.GP;
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(fr + (size_t)y * g.GP);
+        for (int i = threadIdx.x; i < nq; i += 256) {
+            const uint32_t v = s32[i];
+            *reinterpret_cast<float4*>(buf + 4 * i) =
+                make_float4((float)(v & 255), (float)((v >> 8) & 255), (float)((v >> 16) & 255), (float)(v >> 24));
+        }
+        __syncthreads();   // (also: the buffer's previous row, two rows back, is consumed)
+        float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
+#pragma unroll
+        for (int q = 0; q < PH_J; ++q) {
+            const int j = threadIdx.x + 256 * q;
+            if (j >= n2) break;
+            const int c = col[q];
+            float acc = lv.kf[r] * buf[c];
             if (c >= r && c + r < W)   // taps inside the row: reflect101 is the identity
-                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * ((float)s[c - i] + (float)s[c + i]);
+                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (buf[c - i] + buf[c + i]);
             else
                 for (int i = 1; i <= r; ++i)
-                    acc += lv.kf[r + i] * ((float)s[reflect101(c - i, W)] + (float)s[reflect101(c + i, W)]);
+                    acc += lv.kf[r + i] * (buf[reflect101(c - i, W)] + buf[reflect101(c + i, W)]);
+            out[j] = acc;
+        }
+        for (int j = threadIdx.x + 256 * PH_J; j < n2; j += 256) {   // wide levels: taps per row
+            const LinTap tp = lv.xt[j >> 1];
+            const int c = (j & 1) ? tp.s1 : tp.s0;
+            float acc = lv.kf[r] * buf[c];
+            if (c >= r && c + r < W)
+                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (buf[c - i] + buf[c + i]);
+            else
+                for (int i = 1; i <= r; ++i)
+                    acc += lv.kf[r + i] * (buf[reflect101(c - i, W)] + buf[reflect101(c + i, W)]);
             out[j] = acc;
         }
     }
@@ -304,7 +333,10 @@ __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t
 // Vertical smoothing pass (oc_blur_f32, second loop) at the 2h source rows the
 // resize reads: vtmp[2dy][j] at row yt[dy].s0, vtmp[2dy+1][j] at yt[dy].s1, for
 // every column slot j of tmpc — each blurred value the resize needs, once. A
-// workgroup = 256 column slots x PV_ROWS output rows of a frame.
+// workgroup = 256 column slots x PV_ROWS output rows of a frame. The two rows
+// of a level row (s1 = s0 + 1 inside the image) walk their taps together: each
+// step loads the two new outer values and reuses the previous step's (2 loads
+// a tap pair instead of 4; the same sums in the same order).
 constexpr int PV_ROWS = 8;
 __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
 {
@@ -312,8 +344,25 @@ __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
     const int H = g.H, n2 = 2 * lv.w, r = lv.r, yy0 = blockIdx.y * PV_ROWS, yye = min(yy0 + PV_ROWS, 2 * lv.h);
     if (j >= n2) return;
     const float* T = lv.tmpc + (size_t)t * H * n2 + j;
+    float* V = lv.vtmp + (size_t)t * 2 * lv.h * n2 + j;
     for (int yy = yy0; yy < yye; ++yy) {
         const LinTap ty = lv.yt[yy >> 1];
+        if (!(yy & 1) && yy + 1 < yye && ty.s1 == ty.s0 + 1 && ty.s0 >= r && ty.s1 + r < H) {
+            const float* C = T + (uint32_t)(ty.s0 * n2);
+            float lo = C[0], hi = C[n2];   // row s0 - (i-1), row s1 + (i-1)
+            float a0 = lv.kf[r] * lo, a1 = lv.kf[r] * hi;
+            for (int i = 1; i <= r; ++i) {
+                const float lo_i = C[-(int)(i * n2)], hi_i = C[(i + 1) * n2];
+                a0 += lv.kf[r + i] * (lo_i + hi);   // T[s0 - i] + T[s0 + i]
+                a1 += lv.kf[r + i] * (lo + hi_i);   // T[s1 - i] + T[s1 + i]
+                lo = lo_i;
+                hi = hi_i;
+            }
+            V[(size_t)yy * n2] = a0;
+            V[(size_t)(yy + 1) * n2] = a1;
+            ++yy;
+            continue;
+        }
         const int row = (yy & 1) ? ty.s1 : ty.s0;
         float acc = lv.kf[r] * T[(size_t)row * n2];
         if (row >= r && row + r < H) {
@@ -323,7 +372,7 @@ __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
             for (int i = 1; i <= r; ++i)
                 acc += lv.kf[r + i] * (T[(size_t)reflect101(row - i, H) * n2] + T[(size_t)reflect101(row + i, H) * n2]);
         }
-        lv.vtmp[((size_t)t * 2 * lv.h + yy) * n2 + j] = acc;
+        V[(size_t)yy * n2] = acc;
     }
 }
 
@@ -1821,7 +1870,12 @@ __global__ void __launch_bounds__(256) k_of_count_static(OfGeom g, OfBufs B, int
 // --------------------------------------------------------------- launchers --
 static int of_band_rows(const OfGeom& g, size_t* lds)
 {
-    int bh = 8;
+    static const int bh0 = [] {   // DVC_OF_BH (experiments): rows per k_of_band workgroup, 8 / 4 / 2 / 1
+        const char* e = getenv("DVC_OF_BH");
+        const int v = e ? atoi(e) : 8;
+        return v == 4 || v == 2 || v == 1 ? v : 8;
+    }();
+    int bh = bh0;
     for (;;) {
         const size_t b = (size_t)16 * (bh + 4 * (g.mk - 1)) * g.WW + (size_t)16 * bh * g.WW +
                          (size_t)4 * bh * (g.WW + 1) + (size_t)4 * bh * g.CAP + 16;
@@ -1862,7 +1916,7 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 #undef DVC_FRONT0
     }
     for (int k = 1; k <= g.L; ++k) {
-        hipLaunchKernelGGL(k_pyr_h, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)2 * g.GP, s, g, lv[k],
+        hipLaunchKernelGGL(k_pyr_h, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)8 * g.GP, s, g, lv[k],
                            b.gray);
         hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, (2 * lv[k].h + PV_ROWS - 1) / PV_ROWS, n), dim3(256),
                            0, s, g, lv[k]);
