@@ -690,6 +690,16 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
         return v;
     }();
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
+    // The pyramid of batch i also waits for the flow of batch i-1 (not only
+    // i-2, whose R slots it overwrites): a scan launch needs whole CUs (two of
+    // its workgroups fill a CU's register file), so k_of_front0 beside the
+    // coarse levels' latency-bound wavefronts starved both — level 2's first
+    // iteration took ~3 ms beside it for 1.7 % of the pixels. Serial: +4 % (3
+    // rounds, one box). DVC_OF_SERIAL=0 restores the overlap; =2 also holds
+    // the flow of batch i until the mask stage of batch i-1 is done.
+    static const int serial = [] { const char* e = getenv("DVC_OF_SERIAL"); return e ? atoi(e) : 1; }();
+    OfSlot& Sp = h->slot[(h->seq + 1) & 1];   // batch i-1
+    if (serial >= 1 && Sp.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, Sp.ev_flow, 0));
     dvc::SrcFmt sf{};
     {   // 4:2:0 surfaces read in place, or -> BGR (of:66,145) / re-pitched BGR in
         // the slot's frames, read by the pyramid and by k_of_out
@@ -706,6 +716,7 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
     HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_pyr, 0));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_mask, 0));
+    if (serial >= 2 && Sp.recorded) HIP_OK(hipStreamWaitEvent(h->s_flow, Sp.ev_mask, 0));
     if (timed) {
         while (h->ev.size() < h->ev_used + 2) {
             hipEvent_t e;
