@@ -476,15 +476,27 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         tr[k].uy = tabs.size();
         lin_taps(h->lv[k + 1].h, h->lv[k].h, t);
         tabs.insert(tabs.end(), t.begin(), t.end());
-        // k_flow_up stages the coarse rows a workgroup's FU_ROWS rows read in
-        // LDS when they fit (the row taps are monotone: first row's s0 .. last
-        // row's s1)
-        int rows = 0;
-        for (int y0 = 0; y0 < h->lv[k].h; y0 += dvc::FU_ROWS) {
-            const int ye = std::min(y0 + dvc::FU_ROWS, h->lv[k].h) - 1;
-            rows = std::max(rows, t[ye].s1 - t[y0].s0 + 1);
+        // k_flow_up_lds stages the coarse rows a workgroup's up_per rows read
+        // in LDS when they fit (the row taps are monotone: first row's s0 ..
+        // last row's s1); 8 rows a workgroup beat 4 by 0.7% OF and 16 by 0.3%
+        // (3-round same-box A/B), halving the staging per output row
+        static const int up_per = [] {
+            const char* e = getenv("DVC_OF_UP_ROWS");
+            const int v = e ? atoi(e) : dvc::FU_ROWS_LDS;
+            return v >= 1 && v <= 64 ? v : dvc::FU_ROWS_LDS;
+        }();
+        h->lv[k].up_rows = 0;
+        for (int per = up_per; per >= 1 && !h->lv[k].up_rows; per = per > dvc::FU_ROWS ? dvc::FU_ROWS : 0) {
+            int rows = 0;
+            for (int y0 = 0; y0 < h->lv[k].h; y0 += per) {
+                const int ye = std::min(y0 + per, h->lv[k].h) - 1;
+                rows = std::max(rows, t[ye].s1 - t[y0].s0 + 1);
+            }
+            if ((size_t)rows * h->lv[k + 1].w * 8 <= dvc::FU_LDS_MAX) {
+                h->lv[k].up_rows = rows;
+                h->lv[k].up_per = per;
+            }
         }
-        h->lv[k].up_rows = (size_t)rows * h->lv[k + 1].w * 8 <= dvc::FU_LDS_MAX ? rows : 0;
     }
     dvc::LinTap* dtab = nullptr;
     if ((e = of_alloc(h, &dtab, sizeof(dvc::LinTap) * tabs.size())) != hipSuccess) return bad(e, "hipMalloc");

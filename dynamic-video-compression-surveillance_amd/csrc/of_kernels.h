@@ -35,6 +35,7 @@ struct PolyCoef {
     double ig11, ig03, ig33, ig55;
 };
 
+constexpr int FU_ROWS_LDS = 8;           // output rows per k_flow_up_lds workgroup (DVC_OF_UP_ROWS)
 constexpr int FU_ROWS = 4;               // output rows per k_flow_up workgroup
 constexpr size_t FU_LDS_MAX = 48 * 1024;  // k_flow_up_lds: coarse rows staged in LDS, at most this
 
@@ -57,7 +58,8 @@ struct Level {
     float* flow[2];    // ping-pong n x w*h*2 floats
     const LinTap* ux;  // upsample of the coarser level's flow (k < L): w / h entries
     const LinTap* uy;
-    int up_rows;       // most coarse rows a k_flow_up workgroup's rows read (0: stage none in LDS)
+    int up_rows;
+    int up_per;   // output rows per k_flow_up_lds workgroup       // most coarse rows a k_flow_up workgroup's rows read (0: stage none in LDS)
 };
 
 struct OfGeom {

@@ -1941,7 +1941,7 @@ __global__ void __launch_bounds__(256) k_flow_up_lds(FlowArgs A, float* __restri
 {
     extern __shared__ __attribute__((aligned(16))) float2 sup[];
     const int w = A.lv.w, h = A.lv.h, sw = A.sw;
-    const int y0 = blockIdx.y * FU_ROWS, ye = min(y0 + FU_ROWS, h), t = blockIdx.z;
+    const int y0 = blockIdx.y * A.lv.up_per, ye = min(y0 + A.lv.up_per, h), t = blockIdx.z;
     const float* src = A.src + (size_t)t * sw * A.sh * 2;
     const int r0 = A.lv.uy[y0].s0, nr = A.lv.uy[ye - 1].s1 - r0 + 1;   // <= lv.up_rows (host)
     {   // rows r0 .. r0+nr-1: contiguous floats r0*sw*2 ..
@@ -2100,11 +2100,11 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
                     // until iteration 1 writes it), then read it as a flow buffer
                     float* up = L.flow[1];
-                    const dim3 gu(1, (L.h + FU_ROWS - 1) / FU_ROWS, n);
                     if (L.up_rows > 0 && !getenv("DVC_OF_UP_GATHER"))
-                        hipLaunchKernelGGL(k_flow_up_lds, gu, dim3(256), (size_t)L.up_rows * A.sw * 8, s, A, up);
+                        hipLaunchKernelGGL(k_flow_up_lds, dim3(1, (L.h + L.up_per - 1) / L.up_per, n), dim3(256),
+                                           (size_t)L.up_rows * A.sw * 8, s, A, up);
                     else
-                        hipLaunchKernelGGL(k_flow_up, gu, dim3(256), 0, s, A, up);
+                        hipLaunchKernelGGL(k_flow_up, dim3(1, (L.h + FU_ROWS - 1) / FU_ROWS, n), dim3(256), 0, s, A, up);
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
