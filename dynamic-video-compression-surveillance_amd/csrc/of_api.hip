@@ -536,7 +536,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         {(void**)&b.roots, 4 * H * CAP * mb},
         {(void**)&b.nroots, 4 * (size_t)mb},
         {(void**)&b.stats, 8 * 4 * 64},
-        {(void**)&b.scan_ctr, 4 * 8},   // SCAN_Q work-queue counters
+        {(void**)&b.scan_ctr, 4 * 8 * (size_t)(L + 1) * std::max(1, g.iters)},   // SCAN_Q counters a scan launch
         {(void**)&b.scan_abort, 4},
     };
     for (auto& a : allocs)

@@ -104,7 +104,7 @@ struct OfBufs {
     // 64 slots (1 KB, whole 128-B lines) per row block; sized for the largest
     // level by of_scan_slots
     uint32_t* scan_g;
-    unsigned int* scan_ctr;        // work-item counters (SCAN_Q = 8 queues)
+    unsigned int* scan_ctr;        // work-item counters (SCAN_Q = 8 queues) per scan launch of a batch
     unsigned int* scan_abort;      // a hand-off wait timed out
 };
 

@@ -2061,6 +2061,14 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
     }();
     const size_t lds = std::max((size_t)(FL_H + 2 * g.m) * (FL_W + 2 * g.m) * 5 * 4,
                                 (size_t)FL_H * (FL_W + 2 * g.m) * 5 * 8);
+    // every scan launch of this call takes its own set of SCAN_Q work-queue
+    // counters, all zeroed by one fill here: one fill kernel a call instead of
+    // one before each launch (each a dependent launch on the flow stream)
+    int set = 0;
+    if (g.sliding) {
+        const hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4 * SCAN_Q * (size_t)(k_hi - k_lo + 1) * g.iters, s);
+        if (e != hipSuccess) return e;
+    }
     for (int k = k_hi; k >= k_lo; --k) {
         const Level& L = lv[k];
         dim3 grid((L.w + FL_W - 1) / FL_W, (L.h + FL_H - 1) / FL_H, n);
@@ -2094,7 +2102,7 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 S.S = (L.w + sw - 1) / sw;
                 S.NB = (L.h + rb - 1) / rb;
                 S.gpub = b.scan_g;
-                S.next = b.scan_ctr;
+                S.next = b.scan_ctr + SCAN_Q * set++;
                 S.abort = b.scan_abort;
                 S.epoch = ++*epoch;
                 if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
@@ -2108,8 +2116,6 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
-                hipError_t e = hipMemsetAsync(b.scan_ctr, 0, 4 * SCAN_Q, s);
-                if (e != hipSuccess) return e;
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
                 const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
