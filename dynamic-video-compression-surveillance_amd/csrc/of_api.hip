@@ -480,7 +480,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         // in LDS when they fit (the row taps are monotone: first row's s0 ..
         // last row's s1); 8 rows a workgroup beat 4 by 0.7% OF and 16 by 0.3%
         // (3-round same-box A/B), halving the staging per output row
-        static const int up_per = [] {
+        const int up_per = [] {   // read per handle (tests vary it)
             const char* e = getenv("DVC_OF_UP_ROWS");
             const int v = e ? atoi(e) : dvc::FU_ROWS_LDS;
             return v >= 1 && v <= 64 ? v : dvc::FU_ROWS_LDS;

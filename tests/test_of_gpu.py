@@ -342,25 +342,30 @@ def test_compress_with_motion_dropin_chunks(gpu_lib, oracle_lib, tmp_path, monke
 
 @pytest.mark.parametrize("W,H", [(640, 360), (333, 185)])
 def test_of_upsample_forms_agree(gpu_lib, oracle_lib, W, H, monkeypatch):
-    """k_flow_up_lds (coarse rows staged in LDS, the default) and the gather
-    form k_flow_up (DVC_OF_UP_GATHER, the fallback for levels too wide to
-    stage) give the same flow bits, and both equal the oracle's."""
+    """k_flow_up_lds (coarse rows staged in LDS, the default, at 8 output
+    rows a workgroup; 1, 3 and 16 via DVC_OF_UP_ROWS) and the gather form
+    k_flow_up (DVC_OF_UP_GATHER, the fallback for levels too wide to stage)
+    give the same flow bits, and all equal the oracle's."""
     from dvc_amd.synthetic import clip
     frames = clip(W, H, 4, seed=7)
     ref = oracle_lib.OracleOF(W, H)
     ref.prime(frames[0])
     rflows = [ref.step(frames[t])[2] for t in range(1, len(frames))]
     ref.close()
-    for gather in (False, True):
+    for gather, rows in ((False, None), (False, "1"), (False, "3"), (False, "16"), (True, None)):
         if gather:
             monkeypatch.setenv("DVC_OF_UP_GATHER", "1")
         else:
             monkeypatch.delenv("DVC_OF_UP_GATHER", raising=False)
+        if rows:
+            monkeypatch.setenv("DVC_OF_UP_ROWS", rows)
+        else:
+            monkeypatch.delenv("DVC_OF_UP_ROWS", raising=False)
         gpu = gpu_lib.OFWorker(W, H, keep_planes=True)
         gpu.prime(frames[0])
         for t in range(1, len(frames)):
             gpu.step(frames[t])
             f = gpu.flow()
             assert np.array_equal(f.view(np.uint32), rflows[t - 1].view(np.uint32)), \
-                f"gather={gather}: flow differs at frame {t}: {_first_diff(f, rflows[t - 1])}"
+                f"gather={gather} rows={rows}: flow differs at frame {t}: {_first_diff(f, rflows[t - 1])}"
         gpu.close()
