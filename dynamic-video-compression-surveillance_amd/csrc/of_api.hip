@@ -140,6 +140,7 @@ int vote_threshold(double alpha, int L)
 // Events of one batch in flight; two slots alternate (batch i waits on i-2).
 struct OfSlot {
     hipEvent_t ev_pyr = nullptr, ev_flow = nullptr, ev_mask = nullptr;
+    hipEvent_t ev_l1 = nullptr, ev_l0a = nullptr;   // flow: coarse levels done / level 0's first iteration done
     bool recorded = false;
     uint8_t* fin = nullptr;   // staged input: YUV frames converted to BGR, or BGR frames the kernels
                               // cannot read in place, re-pitched (rows of ip), read by the pyramid
@@ -186,7 +187,7 @@ static void of_free(dvc_of* h)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     for (OfSlot& sl : h->slot)
-        for (hipEvent_t e : {sl.ev_pyr, sl.ev_flow, sl.ev_mask})
+        for (hipEvent_t e : {sl.ev_pyr, sl.ev_flow, sl.ev_mask, sl.ev_l1, sl.ev_l0a})
             if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {h->ev_user, h->ev_join})
         if (e) (void)hipEventDestroy(e);
@@ -439,7 +440,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
                 return bad(e, "hipStreamCreate");
     }
     for (OfSlot& sl : h->slot)
-        for (hipEvent_t* ev : {&sl.ev_pyr, &sl.ev_flow, &sl.ev_mask})
+        for (hipEvent_t* ev : {&sl.ev_pyr, &sl.ev_flow, &sl.ev_mask, &sl.ev_l1, &sl.ev_l0a})
             if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     const size_t W = p.width, H = p.height, N = W * H, WW = g.WW, CAP = g.CAP;
     // levels (oc_fb_level_poly geometry)
@@ -711,7 +712,11 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // the flow of batch i until the mask stage of batch i-1 is done.
     static const int serial = [] { const char* e = getenv("DVC_OF_SERIAL"); return e ? atoi(e) : 1; }();
     OfSlot& Sp = h->slot[(h->seq + 1) & 1];   // batch i-1
-    if (serial >= 1 && Sp.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, Sp.ev_flow, 0));
+    // (experiments) =3: wait only for batch i-1's coarse levels, =4: for its
+    // level 0's first iteration — the pyramid then fills the CUs the level-0
+    // scan frees in its tail
+    if (serial >= 1 && Sp.recorded)
+        HIP_OK(hipStreamWaitEvent(h->s_pyr, serial == 3 ? Sp.ev_l1 : serial == 4 ? Sp.ev_l0a : Sp.ev_flow, 0));
     dvc::SrcFmt sf{};
     {   // 4:2:0 surfaces read in place, or -> BGR (of:66,145) / re-pitched BGR in
         // the slot's frames, read by the pyramid and by k_of_out
@@ -737,8 +742,10 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
         }
     }
     if (!(skip & 2)) HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow, &h->epoch));
+    HIP_OK(hipEventRecord(S.ev_l1, h->s_flow));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_flow));
-    if (!(skip & 2)) HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch));
+    if (!(skip & 2))
+        HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch, serial == 4 ? S.ev_l0a : nullptr));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_flow));
         h->ev_used += 2;

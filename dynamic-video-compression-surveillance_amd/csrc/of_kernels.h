@@ -136,7 +136,7 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 // Farneback levels k_hi down to k_lo (L..0 in total, coarse to fine) for frames
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s, unsigned int* epoch);
+                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0 = nullptr);
 // hand-off slots (16 B each) k_flow_scan needs per frame at a level of w x h
 size_t of_scan_slots(const OfGeom& g, int w, int h);
 // vote (frames in order) -> close/open -> 8-CC bounding boxes -> rectangle mask

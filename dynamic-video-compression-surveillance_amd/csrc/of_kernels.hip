@@ -2051,7 +2051,7 @@ size_t of_scan_slots(const OfGeom& g, int w, int h)
 }
 
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s, unsigned int* epoch)
+                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0)
 {
     a0 = reduce_frame(g, a0);
     static const int cus = [] {
@@ -2144,6 +2144,10 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
             } else {
                 hipLaunchKernelGGL(k_flow<0>, grid, dim3(256), lds, s, A);
+            }
+            if (ev_it0 && k == k_lo && it == 0) {   // the caller schedules other work after it
+                const hipError_t e = hipEventRecord(ev_it0, s);
+                if (e != hipSuccess) return e;
             }
         }
     }
