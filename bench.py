@@ -59,6 +59,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # acc>127 bit 1/8 (+ one static bit per block, negligible), write overlay 3 + compressed 3
 BACK_BYTES_PER_PX_FRAME = 9.125
 BACK_BYTES_PER_PX_LAUNCH = 0
+# the fused front (block_size 4, BGR in and out: fd_kernels.h FrontOut) moves the same
+# 9.125 B/px per frame — read BGR 3, write overlay 3 + compressed 3 (speculatively, as
+# static blocks) + motion bits 1/8 — plus, once per launch, prev gray in 1 + gray out 1
+FRONT_FUSED_BYTES_PER_PX_LAUNCH = 2
 PIPE_BYTES_PER_PX = 13         # whole frame: + prev gray 1 read, new gray 1 written
 # OF: k_flow at level 0, per pixel per launch (iterations = 2): read R(prev) 20 + R(cur) 20
 # (+ flow in 8 on the 2nd), write flow 8 on the 1st / the motion bit 1/8 on the 2nd
@@ -154,6 +158,25 @@ def copy_bandwidth(local: int, nbytes=2 << 30, reps=20):
     return max(plain, nt), {"plain": round(plain, 1), "nontemporal": round(nt, 1)}
 
 
+def run_cpu_baseline(args):
+    """One host core (the oracle is single-threaded per feed), and beside it every
+    available core up to the box's CPU share, one feed per core."""
+    W, H = args.width, args.height
+    base = cpu_baseline(W, H, args.cpu_budget, 120, args.path, 1)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count() or 1
+    share = int(os.environ.get("DVC_CPU_SHARE", "16"))
+    ncores = args.cpu_cores or max(1, min(avail, share))
+    if ncores > 1:
+        mc = cpu_baseline(W, H, args.cpu_budget, 120, args.path, ncores)
+        mc["cap"] = (f"{ncores} of {avail} available CPUs: the GPU box's CPU share per GPU is {share} "
+                     f"(DVC_CPU_SHARE)") if ncores < avail else "every available CPU"
+        base["all_cores"] = mc
+    return base
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -190,6 +213,8 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="CPU baseline's multi-core leg: this many feeds on this many host processes (0: every "
                          "available CPU up to the box's CPU share, DVC_CPU_SHARE, default 16)")
+    ap.add_argument("--ktime-seconds", type=float, default=6.0,
+                    help="minimum device time of the hipEvent pass that times the dominant kernel")
     ap.add_argument("--runs", type=int, default=5,
                     help="timed runs of --steps steps each; the line reports the median run (SURVEY.md §8d)")
     args = ap.parse_args()
@@ -203,6 +228,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # the CPU baseline (rank 0 at N=1 only) runs first, in fresh processes, so the
+    # GPU phase below is one contiguous stretch of device work
+    cpu_base = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu_base = run_cpu_baseline(args)
     # DVC_BENCH_ONE_DEVICE=1: rehearse the N > 1 flow on a one-GPU box (every
     # rank on cuda:0, gloo for the end-of-run reduction; RCCL refuses two ranks
     # on one device). The driver's multi-GPU runs never set it.
@@ -324,6 +354,7 @@ def main():
     # (max over ranks per run), all runs listed beside it
     runs = max(1, args.runs)
     elapsed_runs = []
+    st0 = [w.stats() for w in ws]   # counters before the timed runs (prime + warmup)
     for _ in range(runs):
         barrier()
         t0 = time.perf_counter()
@@ -332,39 +363,43 @@ def main():
         t1 = time.perf_counter()
         barrier()
         elapsed_runs.append(t1 - t0)
+    # counters of the timed runs alone (every run steps the same frames): per run
     sts = [w.stats() for w in ws]
-    st = {k: sum(x[k] for x in sts) for k in sts[0]}
+    st = {k: sum(x[k] - x0[k] for x, x0 in zip(sts, st0)) / runs for k in sts[0]}
     for w in ws:
         w.close()
 
-    # dominant kernel: hipEvent-timed launches (k_out on the back stream / k_flow
-    # level 0 on the flow stream) of feed 0 alone, same steps
+    # dominant kernel: hipEvent-timed launches (the fused front on the front
+    # stream or k_out on the back stream / k_flow level 0 on the flow stream) of
+    # feed 0 alone, same steps; at least ~--ktime-seconds of device time, so the
+    # GPU phase is long enough for an outside utilisation sampler to see
     wk = make_worker(0, ktiming=True)
     run_steps([wk], 1)
     wk.ktime(reset=True)
-    ksteps = max(1, min(args.steps, 10))
+    step_s = sorted(elapsed_runs)[len(elapsed_runs) // 2] / max(args.steps, 1)
+    ksteps = max(1, min(args.steps, 10), int(args.ktime_seconds / max(step_s, 1e-6)))
     run_steps([wk], ksteps)
     kms, kn = wk.ktime()
+    kkernel = "k_flow" if of else wk.ktime_kernel()
     wk.close()
     kframes = ksteps * P
 
-    red_dev = "cpu" if one_dev else dev
-    vec = torch.tensor([st["frames"], st["motion_px"], st["components"], st["static_blocks"]],
-                       dtype=torch.float64, device=red_dev)
-    tmax = torch.tensor(elapsed_runs, dtype=torch.float64, device=red_dev)
-    per_rank = torch.zeros(world, dtype=torch.float64, device=red_dev)
-    per_rank[rank] = st["frames"]
-    ranks = {"world_size": 1, "backend": None, "frames_per_rank": [int(st["frames"])]}
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)       # per run: the slowest rank's time
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM)        # RCCL: end-of-run aggregate stats only
-        dist.all_reduce(per_rank, op=dist.ReduceOp.SUM)   # each rank's own frame count
-        ranks = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
-                 "frames_per_rank": [int(x) for x in per_rank.tolist()]}
-    run_times = sorted(float(x) for x in tmax.tolist())
+    # the end-of-run collective (RCCL at N > 1; feeds.reduce_runs): counters
+    # summed, each run's time maxed, every rank's own frame count
+    from dvc_amd.feeds import reduce_runs
+    red = reduce_runs(st, elapsed_runs, rank, world, device="cpu" if one_dev else dev)
+    vec = [red["totals"][k] for k in ("frames", "motion_px", "components", "static_blocks")]
+    tmax = red["run_times_max"]
+    ranks = {"world_size": red["world_size"], "backend": red["backend"], "frames_per_rank": red["frames_per_rank"],
+             "scope": "one timed run"}
+    run_times = sorted(tmax)
     elapsed_max = run_times[len(run_times) // 2] if len(run_times) % 2 else \
         0.5 * (run_times[len(run_times) // 2 - 1] + run_times[len(run_times) // 2])
-    frames_total = args.steps * P * F * world
+    # frames every rank actually stepped in one timed run (the all-reduced
+    # counter), not the nominal steps x P x feeds x world: a short rank is not
+    # over-credited
+    frames_total = float(vec[0])
+    frames_nominal = args.steps * P * F * world
     value = frames_total * W * H / elapsed_max / 1e6
 
     if rank == 0:
@@ -392,14 +427,15 @@ def main():
             traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"),
                                   "k_flow" if args.of_direct else "k_flow_scan", workload, per_launch_frames)
         else:
-            kname = "k_out"
+            kname = kkernel
             per_launch_frames = kframes / max(kn, 1)
             # I420 outputs: 1.5 B/px each instead of 3; 4:2:0 input surfaces are read
             # in place (1.5 B/px instead of the BGR frame's 3)
             back = BACK_BYTES_PER_PX_FRAME - (3.0 if args.out_format == "I420" else 0.0) - (1.5 if yuv else 0.0)
-            bytes_per_launch = (back * kframes + BACK_BYTES_PER_PX_LAUNCH * kn) * W * H / max(kn, 1)
-            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"), "k_out", workload,
-                                  per_launch_frames)
+            per_launch = FRONT_FUSED_BYTES_PER_PX_LAUNCH if kname == "k_front_fused" else BACK_BYTES_PER_PX_LAUNCH
+            bytes_per_launch = (back * kframes + per_launch * kn) * W * H / max(kn, 1)
+            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary.json"),
+                                  "k_front" if kname == "k_front_fused" else "k_out", workload, per_launch_frames)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         # SURVEY §8d's per-pixel bytes for this configuration: frame in (BGR 3 / 4:2:0
         # 1.5), state 4, outputs 2 x (BGR 3 / I420 1.5)
@@ -435,11 +471,12 @@ def main():
                          "frames_per_launch": round(per_launch_frames, 2),
                          "avg_launch_us": round(avg_ms * 1e3, 2), "launches_timed": kn,
                          "timed_with": "feed 0 alone"},
-            "stats": {"frames": int(vec[0]), "motion_px": int(vec[1]), "components": int(vec[2]),
-                      "static_blocks": int(vec[3])},
+            "stats": {"scope": "one timed run, all ranks", "frames": int(vec[0]), "motion_px": int(vec[1]),
+                      "components": int(vec[2]), "static_blocks": int(vec[3]), "frames_nominal": frames_nominal},
             "timing": {"runs": runs, "reported": "median run", "steps_per_run": args.steps,
                        "value_per_run": [round(frames_total * W * H / t / 1e6, 2) for t in
-                                         (float(x) for x in tmax.tolist())]},
+                                         tmax],
+                       "ktime_pass": {"steps": ksteps, "launches": kn}},
             "ranks": ranks,
         }
         if traffic is not None:
@@ -468,22 +505,8 @@ def main():
                                 "hbm": {"achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                         "frac": hbm["frac"], "copy": hbm.get("copy"),
                                         "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"]}}
-        if world == 1 and not args.no_cpu_baseline:
-            # one host core (the oracle is single-threaded per feed), and beside it
-            # every available core up to the box's CPU share, one feed per core
-            base = cpu_baseline(W, H, args.cpu_budget, 120, args.path, 1)
-            try:
-                avail = len(os.sched_getaffinity(0))
-            except Exception:
-                avail = os.cpu_count() or 1
-            share = int(os.environ.get("DVC_CPU_SHARE", "16"))
-            ncores = args.cpu_cores or max(1, min(avail, share))
-            if ncores > 1:
-                mc = cpu_baseline(W, H, args.cpu_budget, 120, args.path, ncores)
-                mc["cap"] = (f"{ncores} of {avail} available CPUs: the GPU box's CPU share per GPU is {share} "
-                             f"(DVC_CPU_SHARE)") if ncores < avail else "every available CPU"
-                base["all_cores"] = mc
-            line["cpu_baseline"] = base
+        if cpu_base is not None:
+            line["cpu_baseline"] = cpu_base
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

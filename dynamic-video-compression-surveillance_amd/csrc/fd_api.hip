@@ -119,6 +119,10 @@ struct Slot {
     uint8_t* fsrc = nullptr;   // YUV frames converted to BGR at the source size, before the resize (pitch sip)
     hipEvent_t ev_front = nullptr, ev_ccl = nullptr, ev_acc = nullptr, ev_out = nullptr;
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
+    // the output bytes its batch writes ([lo, hi) of overlay and compressed; empty
+    // when not requested): a fused front writes outputs before the previous
+    // batches' k_fix have run, so it waits for those that write the same bytes
+    uintptr_t olo[2] = {0, 0}, ohi[2] = {0, 0};
 };
 
 // Batches in flight: three slots.
@@ -189,6 +193,7 @@ struct dvc_fd {
     // dominant-kernel timing
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
+    bool last_fused = false;   // the last batch ran the fused front (KTIMING timed k_front, not k_out)
 };
 
 static void free_all(dvc_fd* h)
@@ -415,6 +420,15 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->g.H = p.height;
     h->g.WW = (p.width + 63) / 64;
     h->g.CAP = p.width / 2 + 1;
+    {   // the contour filter stages a band's run index in LDS: ~32k px per row at most
+        int lds = 160 * 1024;
+        if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 160 * 1024;
+        if (dvc::ccl_max_lds(h->g) > (size_t)lds) {
+            delete h;
+            return fail(DVC_E_UNSUPPORTED, "frame width %d: the contour filter's row index needs %zu B of LDS (max %d)",
+                        p.width, dvc::ccl_max_lds(h->g), lds);
+        }
+    }
     h->gs = (p.width + 3) & ~3;
     h->ip = 3 * h->gs;
     h->sw = p.src_width ? p.src_width : p.width;
@@ -755,9 +769,65 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     dvc::SrcFmt sf{};
     int rc = stage_input(h, S, src, pitch, fstride, n, &d, &dp, &dfs, crows, &sf);
     if (rc) return rc;
+    const int opitch = 3 * h->p.width;
+    const int obytes = (opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
+    const bool out_i420 = h->p.flags & DVC_FLAG_OUT_I420;
+    // fused front (fd_kernels.h FrontOut): block_size 4, BGR frames read in
+    // place or staged, BGR outputs in dword rows; DVC_FD_FUSED=0 turns it off (A/B)
+    static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
+    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && h->B == 4 && sf.fmt == DVC_FMT_BGR &&
+                       !out_i420 && !obytes && (ov || cp);
+    {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
+        const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
+        S.olo[0] = (uintptr_t)ov;
+        S.ohi[0] = ov ? (uintptr_t)ov + span : 0;
+        S.olo[1] = (uintptr_t)cp;
+        S.ohi[1] = cp ? (uintptr_t)cp + span : 0;
+    }
+    dvc::FrontOut fo{};
+    if (fused) {
+        // the speculative stores must not land before an earlier batch's k_fix
+        // rewrites the same bytes: wait for the slot's previous batch (so every
+        // k_fix up to batch i-3 is done, s_out being in order) and for batches
+        // i-1, i-2 where their outputs overlap this one's
+        if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
+        for (int k = 1; k < NSLOT; ++k) {
+            const Slot& P = h->slot[(h->seq + NSLOT - k) % NSLOT];
+            if (!P.recorded) continue;
+            bool overlap = false;
+            for (int u = 0; u < 2; ++u)
+                for (int v = 0; v < 2; ++v)
+                    overlap = overlap || (S.ohi[u] > S.olo[u] && P.ohi[v] > P.olo[v] && S.olo[u] < P.ohi[v] &&
+                                          P.olo[v] < S.ohi[u]);
+            if (overlap) HIP_OK(hipStreamWaitEvent(h->s_front, P.ev_out, 0));
+        }
+        fo.ov = ov;
+        fo.cp = cp;
+        fo.opitch = opitch;
+        fo.ostride = ostride;
+        fo.quant = h->p.quant;
+        fo.qinv = 1.0 / (double)h->p.quant;
+        fo.M = h->M;
+    }
+    // KTIMING: events around the dominant HBM kernel — the fused front on
+    // s_front, else k_out on s_out
+    const bool timed = h->p.flags & DVC_FLAG_KTIMING;
+    if (timed) {
+        while (h->ev.size() < h->ev_used + 2) {
+            hipEvent_t e;
+            HIP_OK(hipEventCreate(&e));
+            h->ev.push_back(e);
+        }
+    }
+    if (timed && fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_front));
     if (!(skip & 1))
         HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
-                                 h->p.ithresh, h->s_front));
+                                 h->p.ithresh, h->s_front, fused ? &fo : nullptr));
+    if (timed && fused) {
+        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_front));
+        h->ev_used += 2;
+    }
+    h->last_fused = fused;
     HIP_OK(hipEventRecord(S.ev_front, h->s_front));
     h->gcur ^= 1;
     HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_front, 0));
@@ -776,10 +846,10 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.ap = h->AP;
     a.overlay = ov;
     a.compressed = cp;
-    a.opitch = 3 * h->p.width;
+    a.opitch = opitch;
     a.ostride = ostride;
-    a.obytes = (a.opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
-    a.out_i420 = (h->p.flags & DVC_FLAG_OUT_I420) ? 1 : 0;
+    a.obytes = obytes;
+    a.out_i420 = out_i420 ? 1 : 0;
     a.kbits = S.c.kbits;
     a.kocc = S.c.kocc;
     a.docc = S.docc;
@@ -812,21 +882,12 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.dbg_dil = h->dbg_dil;
     a.err = h->err;
     a.frame0 = h->frames;
-    // KTIMING: events around k_out (the HBM-bound kernel) on s_out
-    const bool timed = h->p.flags & DVC_FLAG_KTIMING;
-    if (timed) {
-        while (h->ev.size() < h->ev_used + 2) {
-            hipEvent_t e;
-            HIP_OK(hipEventCreate(&e));
-            h->ev.push_back(e);
-        }
-    }
     if (!(skip & 4)) HIP_OK(dvc::launch_accumulate(a, h->s_acc));
     HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
     HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
-    if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
-    if (!(skip & 8)) HIP_OK(dvc::launch_out(a, h->s_out));
-    if (timed) {
+    if (timed && !fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
+    if (!(skip & 8)) HIP_OK(dvc::launch_out(a, h->s_out, fused));
+    if (timed && !fused) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
         h->ev_used += 2;
     }
@@ -1034,6 +1095,12 @@ int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset)
     if (launches) *launches = h->ev_used / 2;
     if (reset) h->ev_used = 0;
     return DVC_OK;
+}
+
+int dvc_fd_ktime_kernel(const dvc_fd* h)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    return h->last_fused ? DVC_KTIME_FRONT_FUSED : DVC_KTIME_OUT;
 }
 
 void dvc_fd_destroy(dvc_fd* h)

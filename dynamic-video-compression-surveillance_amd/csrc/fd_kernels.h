@@ -152,10 +152,30 @@ struct BackArgs {
 // bytes; frames read by the kernels have pitch % 4 == 0 and pitch >= 3 * gs.
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
                         int W, int H, int gs, const GaussTaps& k, hipStream_t s);
+
+// Speculative outputs of the fused front (block_size 4, BGR frames in and out,
+// dword-aligned output rows). A frame is read from HBM once: while k_front has
+// its 4x4 blocks in registers it writes every full block as if it were static —
+// overlay = the frame (no acc > 127 pixel can lie in a block whose acc is all
+// zero, fd:110-111) and compressed = (Y', Y', Y') of the block's quantised DCT
+// (fd:117-130) — and k_fix (k_out<.., FIX>) later rewrites only the blocks the
+// accumulated mask makes non-static (their YCrCb round trip, and the red
+// overlay where acc > 127). Every output byte ends equal to k_out's.
+struct FrontOut {
+    uint8_t* ov;       // nullable; frame t at ov + t * ostride, rows of opitch
+    uint8_t* cp;       // nullable; same layout
+    int opitch;
+    size_t ostride;
+    float quant;
+    double qinv;
+    DctMat M;          // 4 x 4 basis
+};
 // frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
-// gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW
+// gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW;
+// fo (nullable): the fused speculative outputs above
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n, const uint8_t* gray_in,
-                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s);
+                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s,
+                        const FrontOut* fo = nullptr);
 // cv2.resize(frame, (W, H)) INTER_LINEAR 8UC3 (fd:74,91) of n frames into dst
 // (rows of dpitch, frames of dstride). Tables from resize_tables().
 struct ResizeTab {
@@ -170,13 +190,16 @@ void resize_tables(int sw, int sh, int dw, int dh, int* host_x /* 3*dw */, int* 
 hipError_t launch_resize(const uint8_t* src, int spitch, size_t sstride, uint8_t* dst, int dpitch, size_t dstride,
                          int n, const ResizeTab& t, hipStream_t s);
 int band_rows(const RowGeom& g);
+size_t ccl_max_lds(const RowGeom& g);   // dvc_fd_create refuses frames wider than the LDS allows
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
 // k_dilate then k_acc (the accumulated-mask recurrence: batches in order)
 hipError_t launch_accumulate(const BackArgs& a, hipStream_t s);
 // k_out (overlay + compressed frames; no recurrence) and k_out_gen for the
 // generic layout / partial edge blocks (always launched: it also detects the
-// odd-size DCT stop and counts generic static blocks)
-hipError_t launch_out(const BackArgs& a, hipStream_t s);
+// odd-size DCT stop and counts generic static blocks). fix: the fused front
+// wrote every full block speculatively (FrontOut); k_out only rewrites the
+// blocks that are not static.
+hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix = false);
 inline bool fast_block(int B) { return B == 4 || B == 8; }
 
 }  // namespace dvc

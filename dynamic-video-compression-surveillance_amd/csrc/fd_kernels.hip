@@ -122,16 +122,27 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
     }
 }
 
-template <int NW, int PF, int FMT>
-__global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+// OUT (fused speculative outputs, FrontOut in fd_kernels.h; NW = 4, BGR): the
+// rows are dealt by block row instead — wave w loads and owns tile rows
+// 4w..4w+3, so each lane holds one 4x4 block of the frame, plus one halo row
+// (LDS rows 0, 1, 18, 19 for waves 0..3) — and the block's pixels go out as
+// the overlay straight from the registers they were loaded into, its gray
+// quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
+// the compressed frame.
+template <int NW, int PF, int FMT, bool OUT>
+__global__ void __launch_bounds__(64 * NW, OUT ? 4 : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
-                                                   int W, int H, int WW, int ithresh, int xcd_bands)
+                                                   int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
 {
+    static_assert(!OUT || (NW == 4 && FMT == DVC_FMT_BGR), "fused outputs: 16-row tiles of BGR frames");
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // LDS row of this wave's j-th loaded row, and tile row of its i-th output row
+    auto lrow = [&](int j) { return OUT ? (j < 4 ? 2 + 4 * wave + j : (wave < 2 ? wave : 16 + wave)) : wave + NW * j; };
+    auto orow = [&](int i) { return OUT ? 4 * wave + i : wave + NW * i; };
     // XCD bands: blocks b, b+8, .. share an XCD (and its L2); the bijective remap
     // below deals each such group a contiguous run of (chunk, tile row, tile)
     // ids, so a tile's halo rows and halo quads are mostly its own XCD's lines
@@ -165,7 +176,7 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     u16x2 pl[4], ph[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int y = min(y0 + wave + NW * i, H - 1);
+        const int y = min(y0 + orow(i), H - 1);
         const uint32_t v = *reinterpret_cast<const uint32_t*>(gray_in + (size_t)y * gs + xc);
         pl[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c010c00u));
         ph[i] = as_u16x2(__builtin_amdgcn_perm(0u, v, 0x0c030c02u));
@@ -190,7 +201,7 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
         }
     };
 #pragma unroll
-    for (int j = 0; j < NR; ++j) row_off(reflect1(y0 - 2 + min(wave + NW * j, FT_R - 1), H), xc, off[j], coff[j]);
+    for (int j = 0; j < NR; ++j) row_off(reflect1(y0 - 2 + min(lrow(j), FT_R - 1), H), xc, off[j], coff[j]);
     const uint32_t dv = (uint32_t)(sf.voff - sf.uoff);
     const bool halo_wave = __builtin_amdgcn_readfirstlane(wave) < (2 * FT_R + 63) / 64;   // scalar branch
     const bool halo = halo_wave && tid < 2 * FT_R;
@@ -233,11 +244,29 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     const bool fix_r = iW < 4 * FT_Q;
     constexpr int FB = 64 * ((FT_R + 63) / 64);   // first thread of the right fix-up (after the left one's)
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
+    // OUT: this lane's block lies inside the frame (partial edge blocks are
+    // k_out_gen's) and the frame is one of the chunk's (not its warm-up)
+    const bool full_blk = OUT && x + 4 <= W && y0 + 4 * wave + 4 <= H;
+    const size_t orow0 = (size_t)(y0 + 4 * wave) * fo.opitch + 3 * (size_t)x;
     auto frame = [&](Quads& qs, int t) {
 #pragma unroll
         for (int j = 0; j < NR; ++j)
-            if (NR * NW == FT_R || wave + NW * j < FT_R)
-                sg[wave + NW * j][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
+            if (NR * NW == FT_R || lrow(j) < FT_R)
+                sg[lrow(j)][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
+        if constexpr (OUT) {
+            // overlay := the frame (a static block has no acc > 127 pixel); the
+            // registers are reloaded with frame t + PF right after the barrier
+            if (fo.ov && full_blk && t >= t_first) {
+                uint8_t* o = fo.ov + (size_t)t * fo.ostride + orow0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t* r = reinterpret_cast<uint32_t*>(o + (size_t)j * fo.opitch);
+                    __builtin_nontemporal_store(qs.v0[j], r);
+                    __builtin_nontemporal_store(qs.v1[j], r + 1);
+                    __builtin_nontemporal_store(qs.v2[j], r + 2);
+                }
+            }
+        }
         if (halo_wave) {
             const uint32_t gh = quad_gray<FMT>(qs.h0, qs.h1, qs.h2);
             if (halo) sg[hr][hs ? FT_Q - 1 : 0] = gh;
@@ -262,6 +291,13 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
         // frame t + PF into the set just converted (the last frames reload
         // themselves: an unconditional load)
         load(qs, bgr + (size_t)min(t + PF, t_end - 1) * fstride);
+        // OUT: the block's gray quads (this frame's sg is rewritten only after
+        // the barrier below)
+        uint32_t gq[4];
+        if constexpr (OUT) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gq[i] = sg[2 + 4 * wave + i][lane + 1];
+        }
 
 #pragma unroll
         for (int i = 0; i < (FT_R * 64 + NT - 1) / NT; ++i) {
@@ -284,7 +320,7 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
         uint64_t* mb = mbits + (size_t)t * mstride;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int rr = wave + NW * i, y = y0 + rr;
+            const int rr = orow(i), y = y0 + rr;
             const uint2 a0 = sh[rr][lane], a1 = sh[rr + 1][lane], a2 = sh[rr + 2][lane], a3 = sh[rr + 3][lane],
                         a4 = sh[rr + 4][lane];
             // 16-bit lanes: sum <= 16 * 4080 = 65280, packed adds cannot carry across halves
@@ -312,6 +348,31 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
             if ((lane & 7) == 0 && y < H && wi < WW && t >= t_first)
                 reinterpret_cast<uint32_t*>(mb)[((size_t)y * WW + wi) * 2 + ((lane >> 3) & 1)] = w;
         }
+        // OUT: compressed := the block as static (fd:117-130): Y' = trunc(clip(
+        // IDCT(rint(DCT(Y - 128) / q) q) + 128)), Cr = Cb = 128 -> (Y', Y', Y')
+        if constexpr (OUT) {
+            if (fo.cp && full_blk && t >= t_first) {
+                float X[16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) X[4 * i + j] = (float)((int)((gq[i] >> (8 * j)) & 255u) - 128);
+                block_dct_quant_pk<4>(X, fo.M, fo.quant, fo.qinv);
+                uint8_t* o = fo.cp + (size_t)t * fo.ostride + orow0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t u[4], cw[3];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)   // clip to [0, 255], truncating uint8 cast
+                        u[j] = (uint32_t)__builtin_amdgcn_fmed3f(X[4 * i + j] + 128.0f, 0.0f, 255.0f);
+                    gray_bgr4(u[0], u[1], u[2], u[3], cw);
+                    uint32_t* r = reinterpret_cast<uint32_t*>(o + (size_t)i * fo.opitch);
+                    __builtin_nontemporal_store(cw[0], r);
+                    __builtin_nontemporal_store(cw[1], r + 1);
+                    __builtin_nontemporal_store(cw[2], r + 2);
+                }
+            }
+        }
     };
     if constexpr (PF == 2) {
         for (int t = t_begin; t < t_end; t += 2) {
@@ -325,7 +386,7 @@ __global__ void __launch_bounds__(64 * NW) k_front(const uint8_t* __restrict__ b
     if (t_end == n) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int y = y0 + wave + NW * i;
+            const int y = y0 + orow(i);
             if (y < H && x < W)
                 *reinterpret_cast<uint32_t*>(gray_out + (size_t)y * gs + x) =
                     __builtin_amdgcn_perm(as_u32(ph[i]), as_u32(pl[i]), 0x06040200u);
@@ -984,12 +1045,18 @@ __device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, 
 // row, one lane per full BxB block, of frame t of the batch. FMT != BGR: the
 // block's pixels from a 4:2:0 surface (B luma bytes per row, the chroma row of
 // each row pair loaded once), converted to packed BGR in registers.
-template <int B, int FMT>
+// FIX: the fused front already wrote every full block as static (FrontOut);
+// only the blocks that are not static load their pixels and are rewritten —
+// the compressed frame's YCrCb round trip, and the overlay where acc > 127.
+template <int B, int FMT, bool FIX>
 __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int ty, int lane, int wave)
 {
     const int W = a.g.W, H = a.g.H;
     const int bx = tx * 64 * B + lane * B, by = (ty * 4 + wave) * B;
     if (bx + B > W || by + B > H) return;   // partial edge blocks: k_out_gen
+    const bool is_static =
+        (a.sbits[(size_t)t * a.sstride + (size_t)(by / B) * a.SW + (bx / B >> 6)] >> ((bx / B) & 63)) & 1ull;
+    if (FIX && is_static) return;
     const uint8_t* f = a.bgr + (size_t)t * a.fstride;
     uint32_t px[B][3 * B / 4];
     if constexpr (FMT == DVC_FMT_BGR) {
@@ -1029,8 +1096,6 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
             }
         }
     }
-    const bool is_static =
-        (a.sbits[(size_t)t * a.sstride + (size_t)(by / B) * a.SW + (bx / B >> 6)] >> ((bx / B) & 63)) & 1ull;
     // overlay (fd:110-111): (0,0,255) where acc > 127
     if (a.overlay) {
         typedef typename BlkT<B>::T BT;
@@ -1044,6 +1109,7 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
         uint8_t* ovf = a.overlay + (size_t)t * a.ostride;
 #pragma unroll
         for (int i = 0; i < B; ++i) {
+            if (FIX && !rany) break;   // no red pixel: the speculative copy is exact
             uint32_t ow[3 * B / 4];
             if (!rany) {
 #pragma unroll
@@ -1130,14 +1196,14 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
 // Grid-stride over the batch's (frame, tile) pairs with a bounded grid: a few
 // long-lived workgroups per CU keep HBM saturated while leaving wave slots to
 // the latency-bound contour-filter kernels running beside it on other streams.
-template <int B, int FMT>
+template <int B, int FMT, bool FIX>
 __global__ void __launch_bounds__(256) k_out(BackArgs a, int ntx, int nty)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int per = ntx * nty, total = per * a.n;
     for (int u = blockIdx.x; u < total; u += gridDim.x) {   // no barrier in the loop
         const int t = u / per, r = u - t * per, ty = r / ntx;
-        out_tile<B, FMT>(a, t, r - ty * ntx, ty, lane, wave);
+        out_tile<B, FMT, FIX>(a, t, r - ty * ntx, ty, lane, wave);
     }
 }
 
@@ -1437,7 +1503,7 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
 template <int NW>
 static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n,
                             const uint8_t* gray_in, uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g,
-                            int ithresh, hipStream_t s)
+                            int ithresh, hipStream_t s, const FrontOut* fo)
 {
     constexpr int FT_H = 4 * NW;
     const int tx = (g.W + FT_W - 1) / FT_W, ty = (g.H + FT_H - 1) / FT_H;
@@ -1448,34 +1514,62 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     static const int target = [] { const char* e = getenv("DVC_FRONT_WAVES"); return e ? std::max(1, atoi(e)) : 5120; }();
     int chunks = (target / NW + tx * ty / 2) / (tx * ty);
     static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
+    if (fo) {
+        // fused outputs (128 VGPRs: 4 workgroups per CU): every workgroup walks
+        // its frames from first to last, so a grid beyond what is resident at
+        // once would run a second round of whole chunks — as many chunks as
+        // fit (1080p: 544 tiles, 1024 resident -> 1); DVC_FUSED_CHUNKS overrides
+        static const int resident = [] {
+            int dev = 0, cus = 256, per = 4;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                cus = 256;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<4, 1, DVC_FMT_BGR, true>, 256, 0) !=
+                    hipSuccess || per < 1)
+                per = 4;
+            return per * cus;
+        }();
+        static const int fc = [] { const char* e = getenv("DVC_FUSED_CHUNKS"); return e ? atoi(e) : 0; }();
+        chunks = fc > 0 ? fc : resident / (tx * ty);
+    }
     chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
     static const int xcd = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : 0; }();
     static const int pf = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 1; }();
     const dim3 grid(tx, ty, chunks), block(64 * NW);
+    const FrontOut none{};
+    if constexpr (NW == 4) {
+        if (fo) {
+            hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                               gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+            return;
+        }
+    }
     if (sf.fmt == DVC_FMT_I420)
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
-                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else if (sf.fmt == DVC_FMT_NV12)
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
-                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else if (pf == 2)
-        hipLaunchKernelGGL((k_front<NW, 2, DVC_FMT_BGR>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
-                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+        hipLaunchKernelGGL((k_front<NW, 2, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
-                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd);
+        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+                           gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
 }
 
 hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const SrcFmt& sf, int n, const uint8_t* gray_in,
-                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s)
+                        uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s,
+                        const FrontOut* fo)
 {
-    // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16)
+    if (fo && sf.fmt != DVC_FMT_BGR) return hipErrorInvalidValue;   // fused outputs: BGR frames only
+    // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
-    if (nw == 16) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
-    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
-    else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s);
+    if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
+    else if (nw == 8 && !fo) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
+    else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     return hipGetLastError();
 }
 
@@ -1529,6 +1623,14 @@ size_t band_lds(const RowGeom& g, int bh, int budget)
 }
 
 int band_rows(const RowGeom&) { return BAND_ROWS; }
+
+// the largest dynamic LDS any contour-filter launch asks for at this geometry
+// (k_band's run index grows with the row width: 1080p ~14 KB, W ~32k px 160 KB)
+size_t ccl_max_lds(const RowGeom& g)
+{
+    return std::max({band_lds(g, BAND_ROWS, 1024), (size_t)8 * merge_lds_words(g.WW) * (256 / MG),
+                     (size_t)8 * g.WW * CG_ROWS});
+}
 
 // Node budget of a band: 1024 (4 KB of parents beside the run index, ~14 KB
 // per workgroup at 1080p) — bands with more runs and gaps (noise) take the
@@ -1599,7 +1701,7 @@ static void launch_gen(const BackArgs& a, int rx0, int rx1, int ry0, int ry1, in
     hipLaunchKernelGGL(k_out_gen, dim3(R.njx * njy, a.n), dim3(256), lds, s, a, R, fast);
 }
 
-hipError_t launch_out(const BackArgs& a, hipStream_t s)
+hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
 {
     const int B = a.B;
     const int per = std::max(1, 1024 / (B * B));             // blocks of a ~1024-px job
@@ -1625,12 +1727,16 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s)
     const int ntx = (a.g.W + 64 * B - 1) / (64 * B), nty = (a.g.H + 4 * B - 1) / (4 * B);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
     const int f = a.sf.fmt;
-    if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (B == 4) hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<8, DVC_FMT_I420>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<8, DVC_FMT_NV12>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR in and out, dword rows)
+        if (B != 4 || f != DVC_FMT_BGR || a.out_i420 || a.obytes) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    }
+    else if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4) hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<8, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<8, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     return hipGetLastError();
 }
 

@@ -345,7 +345,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         return fail(DVC_E_INVALID, "frame %dx%d outside 8..65520 x >=8", p.width, p.height);
     if (p.morph_kernel < 1 || p.morph_kernel > dvc::OF_MAX_MORPH)
         return fail(DVC_E_UNSUPPORTED, "morph_kernel %d outside 1..%d", p.morph_kernel, dvc::OF_MAX_MORPH);
-    if (p.window < 1 || p.window > 127) return fail(DVC_E_UNSUPPORTED, "window_size %d outside 1..127", p.window);
+    if (p.window < 1 || p.window > 255) return fail(DVC_E_UNSUPPORTED, "window_size %d outside 1..255", p.window);
     if (p.poly_n != 5 && p.poly_n != 7) return fail(DVC_E_UNSUPPORTED, "poly_n %d: 5 or 7", p.poly_n);
     if (p.winsize < 1 || p.winsize / 2 > dvc::OF_MAX_BOX_M)
         return fail(DVC_E_UNSUPPORTED, "winsize %d outside 1..%d", p.winsize, 2 * dvc::OF_MAX_BOX_M + 1);
@@ -398,6 +398,16 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
     dvc_host::dct_matrix(8, h->M);
     ellipse_rows(p.morph_kernel, g);           // of:62
+    {   // the mask stage's morph rows + halo in LDS: a large element on a wide frame may not fit
+        int lds = 160 * 1024;
+        if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 160 * 1024;
+        if (dvc::of_mask_min_lds(g) > (size_t)lds) {
+            const size_t need = dvc::of_mask_min_lds(g);
+            delete h;
+            return fail(DVC_E_UNSUPPORTED, "morph_kernel %d at width %d: the mask stage needs %zu B of LDS (max %d)",
+                        p.morph_kernel, p.width, need, lds);
+        }
+    }
 
     auto bad = [&](hipError_t e, const char* what) {
         int rc = fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "%s: %s", what, hipGetErrorString(e));
@@ -522,7 +532,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         {(void**)&b.gray, (size_t)g.GP * H * mb},
         {(void**)&b.mring, 8 * H * WW * g.RB},
         {(void**)&b.cnt, 64 * H * WW},
-        {(void**)&b.vthr, 256},
+        {(void**)&b.vthr, 2 * 256},
         {(void**)&b.sbits, 8 * H * WW * mb},
         {(void**)&b.obits, 8 * H * WW * mb},
         {(void**)&b.rbits, 8 * H * WW * mb},
@@ -552,10 +562,10 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         if ((e = hipMemset(b.scan_g, 0, 16 * slots * mb)) != hipSuccess) return bad(e, "hipMemset");
     }
     if ((e = hipMemset(b.scan_abort, 0, 4)) != hipSuccess) return bad(e, "hipMemset");
-    uint8_t vt[256];
+    uint16_t vt[256];
     std::memset(vt, 0, sizeof(vt));
-    for (int l = 1; l <= p.window; ++l) vt[l] = (uint8_t)vote_threshold(p.alpha_fraction, l);
-    if ((e = hipMemcpy((void*)b.vthr, vt, 256, hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
+    for (int l = 1; l <= p.window; ++l) vt[l] = (uint16_t)vote_threshold(p.alpha_fraction, l);   // <= l + 1 <= 256
+    if ((e = hipMemcpy((void*)b.vthr, vt, sizeof(vt), hipMemcpyHostToDevice)) != hipSuccess) return bad(e, "hipMemcpy");
     const size_t FS = (size_t)h->ip * H;   // one staged / packed BGR frame
     if (h->fmt != DVC_FMT_BGR)   // BGR device frames: allocated on first use (of_stage), when re-pitched
         for (OfSlot& sl : h->slot)

@@ -26,7 +26,7 @@ constexpr int OF_MAX_LEVELS = 6;
 constexpr int OF_MAX_POLY_N = 7;   // FarnebackPolyExp half-width n = poly_n (5 or 7)
 constexpr int OF_MAX_BOX_M = 8;    // winsize <= 17
 constexpr int OF_MAX_BLUR = 63;    // pyramid smoothing kernel taps
-constexpr int OF_MAX_MORPH = 31;   // morph_kernel (the ellipse's side, of:62)
+constexpr int OF_MAX_MORPH = 64;   // morph_kernel (the ellipse's side, of:62)
 
 // FarnebackPrepareGaussian (optflowgf.cpp), n = poly_n: float taps, index k + n.
 struct PolyCoef {
@@ -84,7 +84,7 @@ struct OfBufs {
     uint8_t* gray;         // n x GP*H, this batch's gray frames (rows of GP)
     uint64_t* mring;       // RB x H*WW raw motion bits (|flow| > thr, of:82-83)
     uint32_t* cnt;         // H x WW*16 u32: vote counts, 4 px (bytes) per u32
-    const uint8_t* vthr;   // vthr[L] = votes needed with L masks in the window (of:86), L <= window
+    const uint16_t* vthr;  // vthr[L] = votes needed with L masks in the window (of:86), L <= window; L+1 = never
     uint64_t* sbits;       // n x H*WW smoothed (vote) bits
     uint64_t* obits;       // n x H*WW after close + open (of:89-90)
     uint64_t* rbits;       // n x H*WW rectangle mask (of:93-97)
@@ -141,6 +141,8 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
 size_t of_scan_slots(const OfGeom& g, int w, int h);
 // vote (frames in order) -> close/open -> 8-CC bounding boxes -> rectangle mask
 hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int window, int n, hipStream_t s);
+// the LDS one row of the mask stage needs (morph_kernel and the width set it): create refuses more than the device has
+size_t of_mask_min_lds(const OfGeom& g);
 // compress_with_motion (of:151-183) + the mask bytes
 hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s);
 // a decoded mask plane (1 or 3 channels, rows of mpitch, frames of mstride) ->

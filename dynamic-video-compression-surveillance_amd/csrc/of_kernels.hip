@@ -275,6 +275,11 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 // loads fly while row y is blurred).
 constexpr int PH_ROWS = 4;
 constexpr int PH_J = 8;   // column slots per thread (n2 <= 256 * PH_J: the taps' columns kept in registers)
+// F32: rows staged as floats, double-buffered (8 x GP bytes of LDS); wide
+// frames (8 x GP > PH_F32_LDS) stage each row as its GP bytes, single-buffered,
+// and convert at the tap (the same float values: (float) of the byte).
+constexpr size_t PH_F32_LDS = 64 * 1024;
+template <bool F32>
 __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t* __restrict__ gray)
 {
     // the row as floats in LDS (each tap one ds_read_b32, no byte convert), the
@@ -295,38 +300,47 @@ __global__ void __launch_bounds__(256) k_pyr_h(OfGeom g, Level lv, const uint8_t
     }
     for (int y = y0; y < ye; ++y) {
         float* buf = srowf + ((y - y0) & 1) * g.GP;
+        uint32_t* bufb = reinterpret_cast<uint32_t*>(srowf);
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(fr + (size_t)y * g.GP);
         for (int i = threadIdx.x; i < nq; i += 256) {
             const uint32_t v = s32[i];
-            *reinterpret_cast<float4*>(buf + 4 * i) =
-                make_float4((float)(v & 255), (float)((v >> 8) & 255), (float)((v >> 16) & 255), (float)(v >> 24));
+            if constexpr (F32)
+                *reinterpret_cast<float4*>(buf + 4 * i) =
+                    make_float4((float)(v & 255), (float)((v >> 8) & 255), (float)((v >> 16) & 255), (float)(v >> 24));
+            else
+                bufb[i] = v;
         }
-        __syncthreads();   // (also: the buffer's previous row, two rows back, is consumed)
+        __syncthreads();   // (F32: also the buffer's previous row, two rows back, is consumed)
+        auto px = [&](int c) -> float {
+            if constexpr (F32) return buf[c];
+            else return (float)reinterpret_cast<const uint8_t*>(bufb)[c];
+        };
         float* out = lv.tmpc + (size_t)t * H * n2 + (size_t)y * n2;
 #pragma unroll
         for (int q = 0; q < PH_J; ++q) {
             const int j = threadIdx.x + 256 * q;
             if (j >= n2) break;
             const int c = col[q];
-            float acc = lv.kf[r] * buf[c];
+            float acc = lv.kf[r] * px(c);
             if (c >= r && c + r < W)   // taps inside the row: reflect101 is the identity
-                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (buf[c - i] + buf[c + i]);
+                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (px(c - i) + px(c + i));
             else
                 for (int i = 1; i <= r; ++i)
-                    acc += lv.kf[r + i] * (buf[reflect101(c - i, W)] + buf[reflect101(c + i, W)]);
+                    acc += lv.kf[r + i] * (px(reflect101(c - i, W)) + px(reflect101(c + i, W)));
             out[j] = acc;
         }
         for (int j = threadIdx.x + 256 * PH_J; j < n2; j += 256) {   // wide levels: taps per row
             const LinTap tp = lv.xt[j >> 1];
             const int c = (j & 1) ? tp.s1 : tp.s0;
-            float acc = lv.kf[r] * buf[c];
+            float acc = lv.kf[r] * px(c);
             if (c >= r && c + r < W)
-                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (buf[c - i] + buf[c + i]);
+                for (int i = 1; i <= r; ++i) acc += lv.kf[r + i] * (px(c - i) + px(c + i));
             else
                 for (int i = 1; i <= r; ++i)
-                    acc += lv.kf[r + i] * (buf[reflect101(c - i, W)] + buf[reflect101(c + i, W)]);
+                    acc += lv.kf[r + i] * (px(reflect101(c - i, W)) + px(reflect101(c + i, W)));
             out[j] = acc;
         }
+        if constexpr (!F32) __syncthreads();   // single buffer: every tap read before the next row lands
     }
 }
 
@@ -882,27 +896,41 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
 
 // Hand-off between strips: per (frame, strip, row block) the state of every
 // (row, channel) chain after the strip's last column, as one 16-byte slot
-// {epoch, double lo, double hi, epoch} written by one buffer_store_dwordx4 sc1
-// (write-through past the XCD's L2) and read by buffer_load_dwordx4 sc1 (past
-// L1) polls until both tags equal the launch's epoch. A slot is its own flag:
-// no separate flag store, no drain of the payload stores before it, one
-// round trip for the consumer instead of flag + payload. 16-B sc1 stores are
-// observed untorn on gfx950 (MI355X_MICROARCH.md, hand-off section: not an
-// architectural guarantee) and the two tags bracket the value, so a torn read
-// — a half from another launch — fails the tag test and is re-polled instead
-// of used. Every slot is written once per launch and a row block's 60 slots
-// fill whole 128-B lines of their own. A poll that ever exceeds ~1 s sets
-// `abort` (reported by the host as an error) instead of hanging.
+// {tag_a, lo, hi, tag_b} (the f64 as two dwords) written by one
+// buffer_store_dwordx4 sc1 (write-through past the XCD's L2) and read by
+// buffer_load_dwordx4 sc1 (past L1) polls. A slot is its own flag: no separate
+// flag store, no drain of the payload stores before it, one round trip for the
+// consumer instead of flag + payload. The tags carry the launch's epoch FOLDED
+// WITH THE PAYLOAD (slot_tags): tag_a = epoch ^ lo ^ rotl(hi, 13), tag_b =
+// epoch ^ hi ^ rotl(lo, 7), and a read is accepted only when both tags match the
+// epoch and the lo / hi it read together. So the protocol does not rest on the
+// 16-B store being untorn: a read that mixes dwords of this launch's store with
+// an older launch's (or never-written memory) fails the check and is re-polled
+// unless the mixed-in dwords equal the new ones anyway — accepting a wrong value
+// needs both tags to collide, i.e. an old and a new payload whose XOR is one of
+// 15 fixed bit patterns AND a torn read of exactly that slot. Every slot is
+// written once per launch and a row block's 60 slots fill whole 128-B lines of
+// their own. A poll that ever exceeds ~1 s sets `abort` (reported by the host
+// as an error) instead of hanging.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int SCAN_RSRC_W3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int CPOL_SC1 = 16;               // gfx940+ cache policy bit: sc1
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// the slot of value bits (lo, hi) published in launch `epoch`
+__device__ __forceinline__ u32x4 slot_tags(uint32_t epoch, uint32_t lo, uint32_t hi)
+{
+    return u32x4{epoch ^ lo ^ rotl32(hi, 13), lo, hi, epoch ^ hi ^ rotl32(lo, 7)};
+}
 
 __device__ __forceinline__ bool scan_poll(const ScanArgs& S, __amdgpu_buffer_rsrc_t r, uint32_t off, double& v)
 {
     unsigned spins = 0;
     for (;;) {
         const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CPOL_SC1);
-        if (q.x == S.epoch && q.w == S.epoch) {
+        const u32x4 e = slot_tags(S.epoch, q.y, q.z);
+        if (q.x == e.x && q.w == e.w) {
             v = __builtin_bit_cast(double, (unsigned long long)q.y | ((unsigned long long)q.z << 32));
             return true;
         }
@@ -1152,7 +1180,7 @@ __device__ void scan_strip(const ScanArgs& S, int t, int s, float* sM, double* s
                 }
                 if (s + 1 < S.S) {   // the state after the strip's last column, for the right strip
                     const unsigned long long bits = __builtin_bit_cast(unsigned long long, acc);
-                    const u32x4 q = {S.epoch, (uint32_t)bits, (uint32_t)(bits >> 32), S.epoch};
+                    const u32x4 q = slot_tags(S.epoch, (uint32_t)bits, (uint32_t)(bits >> 32));
                     __builtin_amdgcn_raw_buffer_store_b128(q, r_mine, (uint32_t)(yb * 64 + tid) * 16u, 0, CPOL_SC1);
                 }
             }
@@ -1382,13 +1410,16 @@ __global__ void __launch_bounds__(256) k_vote(OfGeom g, OfBufs b, long long a0, 
         const uint32_t ow = a - window >= 1 ? mr[(size_t)ring(a - window, g.RB) * plane16 + cc] : 0u;
         const int L = (int)min<long long>(a, (long long)window);
         const uint32_t thr = b.vthr[L];
-        const uint32_t bias = (0x80u - thr) * 0x01010101u;
+        // count >= thr per byte (counts and thresholds 0..255, window <= 255): the
+        // even and the odd bytes as u16 lanes plus 256 - thr, bit 8 of each lane
+        const uint32_t bias = (0x100u - thr) * 0x00010001u;
         uint32_t out = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            // bytes stay exact: the u32 sum is linear and every final byte is a count <= window
             cnt[j] = cnt[j] + spread((nw >> (4 * j)) & 15u) - spread((ow >> (4 * j)) & 15u);
-            const uint32_t ge = (cnt[j] + bias) & 0x80808080u;   // count <= 127, thr <= 128: no carries
-            out |= (((ge >> 7) & 1u) | ((ge >> 14) & 2u) | ((ge >> 21) & 4u) | ((ge >> 28) & 8u)) << (4 * j);
+            const uint32_t ge = (cnt[j] & 0x00ff00ffu) + bias, go = ((cnt[j] >> 8) & 0x00ff00ffu) + bias;
+            out |= (((ge >> 8) & 1u) | ((go >> 7) & 2u) | ((ge >> 22) & 4u) | ((go >> 21) & 8u)) << (4 * j);
         }
         nmot += (unsigned long long)__popc(nw);
         if (act) sb[(size_t)t * plane16 + c] = (uint16_t)out;
@@ -1868,6 +1899,16 @@ __global__ void __launch_bounds__(256) k_of_count_static(OfGeom g, OfBufs B, int
 }
 
 // --------------------------------------------------------------- launchers --
+// k_of_band's dynamic LDS at `bh` rows a workgroup: the morph rows with their
+// 4 (mk - 1) halo rows, the run index, the parents
+static size_t of_band_lds(const OfGeom& g, int bh)
+{
+    return (size_t)16 * (bh + 4 * (g.mk - 1)) * g.WW + (size_t)16 * bh * g.WW + (size_t)4 * bh * (g.WW + 1) +
+           (size_t)4 * bh * g.CAP + 16;
+}
+
+size_t of_mask_min_lds(const OfGeom& g) { return of_band_lds(g, 1); }
+
 static int of_band_rows(const OfGeom& g, size_t* lds)
 {
     static const int bh0 = [] {   // DVC_OF_BH (experiments): rows per k_of_band workgroup, 8 / 4 / 2 / 1
@@ -1877,8 +1918,7 @@ static int of_band_rows(const OfGeom& g, size_t* lds)
     }();
     int bh = bh0;
     for (;;) {
-        const size_t b = (size_t)16 * (bh + 4 * (g.mk - 1)) * g.WW + (size_t)16 * bh * g.WW +
-                         (size_t)4 * bh * (g.WW + 1) + (size_t)4 * bh * g.CAP + 16;
+        const size_t b = of_band_lds(g, bh);
         if (b <= 150 * 1024 || bh == 1) {
             *lds = b;
             return bh;
@@ -1888,7 +1928,7 @@ static int of_band_rows(const OfGeom& g, size_t* lds)
 }
 
 // Frame numbers as the kernels see them: a0 itself up to RED_K (so the vote's
-// `a - window >= 1` and `min(a, window)` read the true values; window <= 127),
+// `a - window >= 1` and `min(a, window)` read the true values; window <= 255),
 // beyond it RED_K + (a0 - RED_K) mod lcm(RS, RB) — the same slot in both rings.
 static constexpr long long RED_K = 256;
 static long long reduce_frame(const OfGeom& g, long long a0)
@@ -1916,8 +1956,12 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
 #undef DVC_FRONT0
     }
     for (int k = 1; k <= g.L; ++k) {
-        hipLaunchKernelGGL(k_pyr_h, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)8 * g.GP, s, g, lv[k],
-                           b.gray);
+        if ((size_t)8 * g.GP <= PH_F32_LDS)
+            hipLaunchKernelGGL(k_pyr_h<true>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)8 * g.GP, s, g,
+                               lv[k], b.gray);
+        else   // wide frames: byte rows (GP <= 65520 B of LDS)
+            hipLaunchKernelGGL(k_pyr_h<false>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)g.GP, s, g,
+                               lv[k], b.gray);
         hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, (2 * lv[k].h + PV_ROWS - 1) / PV_ROWS, n), dim3(256),
                            0, s, g, lv[k]);
         dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);

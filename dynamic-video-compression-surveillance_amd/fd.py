@@ -55,7 +55,7 @@ def derive_params(width: int, height: int, block_size: int = 4, motion_threshold
 class FDWorker:
     def __init__(self, width: int, height: int, *, device: int = 0, stream=None,
                  device_ptrs: bool = False, keep_planes: bool = False, ktiming: bool = False,
-                 max_batch: int = 1, out_format: str = "BGR", **kwargs):
+                 max_batch: int = 1, out_format: str = "BGR", fused: bool = True, **kwargs):
         """``width, height``: the scaled frame size (fd:60-61); frames handed to
         :meth:`prime`/:meth:`step` are ``src_width x src_height`` (the video's,
         default the same) and are resized on the GPU (fd:74,91).
@@ -66,12 +66,14 @@ class FDWorker:
         dvc_fd_create documents. ``in_format`` (kwarg) "BGR" / "I420" / "NV12":
         the frames handed over (4:2:0 decoder surfaces are converted on the GPU);
         ``out_format`` "BGR" or "I420": overlay and compressed frames as the
-        encoder's 4:2:0 input (DVC_FLAG_OUT_I420)."""
+        encoder's 4:2:0 input (DVC_FLAG_OUT_I420). ``fused=False``: outputs in
+        one k_out pass instead of the fused front's speculative static-block
+        outputs + k_fix (DVC_FLAG_FD_UNFUSED; same bytes)."""
         if out_format not in ("BGR", "I420"):
             raise ValueError(f"out_format {out_format!r}: BGR or I420")
         flags = (N.DVC_FLAG_DEVICE_PTRS if device_ptrs else 0) | (N.DVC_FLAG_KEEP_PLANES if keep_planes else 0) \
             | (N.DVC_FLAG_KTIMING if ktiming else 0) | (N.DVC_FLAG_JOIN_STREAM if stream is not None else 0) \
-            | (N.DVC_FLAG_OUT_I420 if out_format == "I420" else 0)
+            | (N.DVC_FLAG_OUT_I420 if out_format == "I420" else 0) | (0 if fused else N.DVC_FLAG_FD_UNFUSED)
         self.out_format = out_format
         self.params = derive_params(width, height, flags=flags, **kwargs)
         self.params.max_batch = int(max_batch)
@@ -193,11 +195,19 @@ class FDWorker:
         return out
 
     def ktime(self, reset: bool = False):
-        """(total ms, launches) of the dominant (back) kernel, hipEvent-timed."""
+        """(total ms, launches) of the dominant HBM kernel, hipEvent-timed."""
         ms = ctypes.c_double()
         n = ctypes.c_uint64()
         N.check(self._lib.dvc_fd_ktime(self._h, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0))
         return float(ms.value), int(n.value)
+
+    def ktime_kernel(self) -> str:
+        """Which kernel ktime() timed in the last batch: "k_front_fused" (the fused
+        front with the speculative outputs) or "k_out"."""
+        k = self._lib.dvc_fd_ktime_kernel(self._h)
+        if k < 0:
+            N.check(k)
+        return "k_front_fused" if k == N.KTIME_FRONT_FUSED else "k_out"
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -52,6 +52,30 @@ def aggregate(stats: dict, elapsed_s: float | None = None, device=None) -> dict:
     return out
 
 
+def reduce_runs(stats: dict, run_times: Sequence[float], rank: int, world: int, device=None) -> dict:
+    """bench.py's end-of-run collective: three float64 all-reduces when a
+    process group is up (RCCL on device tensors at N > 1) — the counters summed
+    over ranks, each timed run's wall time maxed (the slowest rank bounds the
+    run), and every rank's own frame count (a zero vector with this rank's slot
+    set, summed). Identity without a process group."""
+    import torch
+    import torch.distributed as dist
+    vec = torch.tensor([float(stats.get(k, 0)) for k in STAT_KEYS], dtype=torch.float64, device=device)
+    tmax = torch.tensor([float(t) for t in run_times], dtype=torch.float64, device=device)
+    per_rank = torch.zeros(max(world, 1), dtype=torch.float64, device=device)
+    per_rank[rank] = float(stats.get("frames", 0))
+    up = dist.is_available() and dist.is_initialized()
+    if up:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)       # per run: the slowest rank's time
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)        # end-of-run aggregate stats only
+        dist.all_reduce(per_rank, op=dist.ReduceOp.SUM)   # each rank's own frame count
+    return {"totals": {k: float(v) for k, v in zip(STAT_KEYS, vec.tolist())},
+            "run_times_max": [float(x) for x in tmax.tolist()],
+            "frames_per_rank": [int(round(x)) for x in per_rank.tolist()],
+            "world_size": dist.get_world_size() if up else 1,
+            "backend": dist.get_backend() if up else None}
+
+
 def process_feeds(video_paths: Iterable[str], output_dir: str, technique: str = "Frame Differencing",
                   **kwargs) -> list:
     """Run this rank's shard of ``video_paths`` through the reference-compatible

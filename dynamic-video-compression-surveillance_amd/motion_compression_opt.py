@@ -13,9 +13,12 @@ Same public surface, kwargs, defaults, return values and side effects:
 
 Videos are mp4v through OpenCV when it is importable, else ``.npy`` frame
 streams of the same basename (``video_io``); with the lossless streams the
-two passes give exactly the fused worker's output. Errors are logged and the
-functions return ``(0, 0, 0)`` / ``None`` as the reference does
-(``of:40-42, 55-58, 123-128``).
+two passes give exactly the fused worker's output. Error convention as the
+reference's: a video that cannot be opened, or a first frame that cannot be
+read, is logged and the function returns ``(0, 0, 0)`` (``of:40-42, 55-58,
+123-128``); an error inside either frame loop propagates to the caller, since
+neither ``of:65-101`` nor ``of:141-185`` has a ``try`` (outputs are still
+released on the way out).
 
 The per-frame work runs on the GPU: ``OFWorker`` (Farneback, vote, close/open,
 rectangles; of:70-97) and ``OFCompressor`` / ``dvc_ofc_run`` (of:141-185) —
@@ -113,9 +116,7 @@ def temporal_smoothing_flow(video_path, output_dir, flow_threshold=0.5, alpha_fr
             if n < R:
                 break
         pipe.finish()
-    except Exception as e:
-        logging.error(f"Error during motion detection: {e}", exc_info=True)
-    finally:
+    finally:   # of:65-101 has no try: an error propagates to the caller (outputs are still released here)
         if pipe is not None:
             pipe.stop()
         cap.release()
@@ -189,9 +190,7 @@ def compress_with_motion(input_video, mask_video, output_dir, quantization_level
                 if n < R:
                     break
             pipe.finish()
-    except Exception as e:
-        logging.error(f"Error during compression: {e}", exc_info=True)
-    finally:
+    finally:   # of:141-185 has no try either: errors propagate
         if pipe is not None:
             pipe.stop()
         if comp is not None:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DVC_ABI_VERSION 6
+#define DVC_ABI_VERSION 7
 #define DVC_MAX_BATCH 512
 
 /* ---- status codes ---------------------------------------------------------- */
@@ -77,6 +77,16 @@ extern "C" {
                                      U and V planes of W/2 x H/2; out_stride >=
                                      W*H*3/2). block_size 4 or 8, W and H
                                      multiples of it (else DVC_E_UNSUPPORTED)  */
+
+#define DVC_FLAG_FD_UNFUSED  0x40u /* FD: write the outputs in one k_out pass after
+                                     the accumulated mask instead of the fused
+                                     front's speculative static-block outputs +
+                                     k_fix (same bytes; the fused form reads each
+                                     frame from HBM once instead of twice. It
+                                     applies to block_size 4, BGR frames in and
+                                     out, 4-byte aligned output rows; the
+                                     environment variable DVC_FD_FUSED=0 sets
+                                     this flag for every handle)                */
 
 /* ---- frame formats (video I/O) ----------------------------- */
 /* What the worker's frames are. The reference's are packed BGR straight from
@@ -266,9 +276,18 @@ int dvc_fd_get_stats(dvc_fd* h, dvc_fd_stats* out);
 int dvc_fd_read_plane(dvc_fd* h, int plane, uint8_t* host_dst);
 
 /* With DVC_FLAG_KTIMING: total milliseconds and launch count of the dominant
- * HBM-bound kernel (k_out: overlay + compress, one launch per batch) since the
- * last reset (synchronises the handle). reset!=0 clears. */
+ * HBM-bound kernel (one launch per batch: the fused front — gray, blur,
+ * threshold and the speculative overlay / compressed frames — where the batch
+ * ran it, else k_out: overlay + compress) since the last reset (synchronises
+ * the handle). reset!=0 clears. */
 int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
+
+/* Which kernel dvc_fd_ktime timed in the last batch: DVC_KTIME_OUT (k_out) or
+ * DVC_KTIME_FRONT_FUSED (k_front with the fused outputs: block_size 4, BGR
+ * frames in and out, 4-byte aligned output rows). Negative on error. */
+#define DVC_KTIME_OUT 0
+#define DVC_KTIME_FRONT_FUSED 1
+int dvc_fd_ktime_kernel(const dvc_fd* h);
 
 void dvc_fd_destroy(dvc_fd* h);
 

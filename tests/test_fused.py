@@ -1,0 +1,115 @@
+"""GPU parity of the fused front (fd_kernels.h FrontOut) against the one-pass
+output stage, through the C-ABI.
+
+With block_size 4 and BGR frames in and out, k_front writes every full 4x4
+block of both outputs as if it were static (overlay = the frame, compressed =
+(Y', Y', Y') of the quantised DCT, frame_differencing.py:110-130) while it has
+the frame in registers, and k_fix rewrites the blocks the accumulated mask
+makes non-static. The bytes must equal the unfused k_out pass
+(DVC_FLAG_FD_UNFUSED) and the oracle, including when a caller reuses output
+buffers across calls — a later batch's speculative stores must not land
+before an earlier batch's k_fix of the same bytes.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames_dev(W, H, n, seed, noisy, dev):
+    import torch
+    from dvc_amd.synthetic import clip
+    fr = clip(W, H, n, seed=seed, noisy=noisy)
+    return fr, torch.from_numpy(fr).to(dev)
+
+
+@pytest.mark.parametrize("W,H,n,batch,seed,noisy", [
+    (1920, 1080, 121, 40, 3, False),
+    (640, 360, 61, 20, 4, True),
+    (644, 362, 41, 13, 5, False),     # partial edge blocks: k_out_gen beside the fused front
+    (1000, 200, 33, 32, 6, True),     # W % 256 != 0: tiles that run past the frame's right edge
+])
+def test_fused_equals_unfused(gpu_lib, W, H, n, batch, seed, noisy):
+    """Every output frame of the fused path == the one-pass k_out path, batched."""
+    import torch
+    dev = torch.device("cuda", 0)
+    _, seq = _frames_dev(W, H, n, seed, noisy, dev)
+    outs = {}
+    for fused in (True, False):
+        w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=batch, fused=fused, ktiming=True)
+        w.prime(seq[0])
+        ov = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device=dev)
+        cp = torch.empty_like(ov)
+        w.step_batch(seq[1:], ov, cp)
+        w.sync()
+        assert w.ktime_kernel() == ("k_front_fused" if fused else "k_out")
+        outs[fused] = (ov, cp, w.stats())
+        w.close()
+    (ovf, cpf, sf), (ovu, cpu_, su) = outs[True], outs[False]
+    assert sf == su
+    for t in range(n - 1):
+        assert torch.equal(ovf[t], ovu[t]), f"overlay: fused != unfused at frame {t + 1}"
+        assert torch.equal(cpf[t], cpu_[t]), f"compressed: fused != unfused at frame {t + 1}"
+
+
+def test_fused_one_output(gpu_lib):
+    """Only one of the outputs requested: the other pointer is NULL in both kernels."""
+    import torch
+    dev = torch.device("cuda", 0)
+    W, H, n = 640, 360, 25
+    _, seq = _frames_dev(W, H, n, 8, False, dev)
+    ref = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=8, fused=False)
+    ref.prime(seq[0])
+    rov = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device=dev)
+    rcp = torch.empty_like(rov)
+    ref.step_batch(seq[1:], rov, rcp)
+    ref.sync()
+    ref.close()
+    for which in ("overlay", "compressed"):
+        w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=8)
+        w.prime(seq[0])
+        out = torch.empty_like(rov)
+        if which == "overlay":
+            w.step_batch(seq[1:], out, None)
+        else:
+            w.step_batch(seq[1:], None, out)
+        w.sync()
+        w.close()
+        assert torch.equal(out, rov if which == "overlay" else rcp), which
+
+
+def test_fused_reused_output_buffers(gpu_lib, oracle_lib):
+    """The bench's pattern and a ring-buffer caller's: chunks of frames stepped
+    into TWO output buffers in turn with no sync between calls, so batch k
+    writes the bytes batch k-2 wrote (and its k_fix rewrote). Different motion
+    in every chunk: a stale k_fix landing after the next speculative stores
+    would leave non-static blocks of the wrong frame. The final contents of both
+    buffers must equal the per-frame unfused run and the oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    W, H, chunk, chunks = 640, 360, 9, 7
+    n = 1 + chunk * chunks
+    frames, seq = _frames_dev(W, H, n, 9, True, dev)
+    ring = [(torch.empty((chunk, H, W, 3), dtype=torch.uint8, device=dev),
+             torch.empty((chunk, H, W, 3), dtype=torch.uint8, device=dev)) for _ in range(2)]
+    w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=chunk)
+    w.prime(seq[0])
+    for c in range(chunks):
+        ov, cp = ring[c % 2]
+        w.step_batch(seq[1 + c * chunk:1 + (c + 1) * chunk], ov, cp)
+    w.sync()
+    w.close()
+    # reference: the oracle frame by frame; the last two chunks' outputs
+    ref = oracle_lib.OracleFD(W, H)
+    ref.prime(frames[0])
+    last = {}
+    for t in range(1, n):
+        rov, rcp, _ = ref.step(frames[t])
+        c, j = divmod(t - 1, chunk)
+        if c >= chunks - 2:
+            last[(c, j)] = (rov, rcp)
+    ref.close()
+    for (c, j), (rov, rcp) in last.items():
+        ov, cp = ring[c % 2]
+        assert np.array_equal(ov[j].cpu().numpy(), rov), f"overlay != oracle: chunk {c} frame {j}"
+        assert np.array_equal(cp[j].cpu().numpy(), rcp), f"compressed != oracle: chunk {c} frame {j}"
