@@ -392,10 +392,15 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
         return fail(DVC_E_INVALID, "frame %dx%d outside 16..65520 x >=16", p.width, p.height);
     if (p.src_width < 0 || p.src_height < 0 || p.src_width > 65520)
         return fail(DVC_E_INVALID, "source frame %dx%d invalid", p.src_width, p.src_height);
-    if (p.block < 1 || p.block > 64)
-        return fail(DVC_E_UNSUPPORTED, "block_size %d: the GPU path implements 1..64", p.block);
-    if (p.ksize < 1 || p.ksize > 63 || p.anchor < 0 || p.anchor >= p.ksize)
-        return fail(DVC_E_INVALID, "dilation kernel %d (anchor %d) outside 1..63", p.ksize, p.anchor);
+    // block_size: k_out_gen stages a block's two B x B float planes in LDS (B = 128: 128 KB);
+    // kernel_size: the dilation shifts a row by at most 63 bits either way (anchor k/2)
+    if (p.block < 1 || p.block > 128)
+        return fail(DVC_E_UNSUPPORTED, "block_size %d: the GPU path implements 1..128", p.block);
+    if (p.ksize < 1 || p.anchor < 0 || p.anchor >= p.ksize)
+        return fail(DVC_E_INVALID, "dilation kernel %d (anchor %d) invalid", p.ksize, p.anchor);
+    if (p.anchor > 63 || p.ksize - 1 - p.anchor > 63)
+        return fail(DVC_E_UNSUPPORTED, "dilation kernel %d (anchor %d): the GPU path implements 1..127", p.ksize,
+                    p.anchor);
     if (p.ithresh < -1 || p.ithresh > 255) return fail(DVC_E_INVALID, "ithresh %d outside -1..255", p.ithresh);
     if (!(p.quant == p.quant) || p.quant == 0.0f) return fail(DVC_E_INVALID, "quantization_level must be nonzero");
     if (p.in_format != DVC_FMT_BGR && p.in_format != DVC_FMT_I420 && p.in_format != DVC_FMT_NV12)

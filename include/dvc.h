@@ -130,15 +130,17 @@ int dvc_bgr_to_i420(const uint8_t* bgr, size_t bgr_pitch, size_t bgr_stride, int
  *                 video's, fd:57-58); 0 = width,height. When they differ the
  *                 worker resizes every frame on the GPU first (cv2.resize
  *                 INTER_LINEAR 8U, fd:74,91).
- *   block         block_size (fd:22), 1..64; partial blocks at the right and
- *                 bottom edges are their slices (fd:117-127).
+ *   block         block_size (fd:22), 1..128 (DVC_E_UNSUPPORTED above: a
+ *                 static block's DCT planes are staged in LDS); partial blocks
+ *                 at the right and bottom edges are their slices (fd:117-127).
  *   ithresh       floor(motion_threshold): cv::threshold on 8U floors the
  *                 threshold, so motion = absdiff > ithresh (fd:97).
  *   min_area2     floor(2*min_area): a contour is kept iff 2*area > min_area2,
  *                 which is contourArea(c) > min_area exactly, because 2*area of
  *                 an integer-vertex polygon is an integer (fd:103).
  *   ksize,anchor  dilation kernel np.ones((k,k)) with OpenCV's default anchor
- *                 k/2 (fd:80,106). 1 <= ksize <= 63.
+ *                 k/2 (fd:80,106). 1 <= ksize <= 127 (DVC_E_UNSUPPORTED above:
+ *                 a row is dilated by word shifts of at most 63 bits).
  *   alpha,beta,gamma  addWeighted weights as float32: release_factor,
  *                 1-release_factor, 0 (fd:107).
  *   quant         quantization_level as float32 (fd:123).
@@ -345,9 +347,10 @@ typedef struct dvc_of_stats {
     uint64_t static_blocks; /* full 8x8 blocks with an all-zero mask (of:161)   */
 } dvc_of_stats;
 
-/* Create an OF feed handle on `device` (GPU constraints: width and height
- * multiples of 8, morph_kernel 2, poly_n 5 or 7, winsize <= 17, window <= 127,
- * pyramid smoothing kernels <= 63 taps). Replaces the per-video setup at
+/* Create an OF feed handle on `device` (GPU constraints, DVC_E_UNSUPPORTED
+ * outside them: width and height >= 8, morph_kernel 1..64 (and its halo rows
+ * within the LDS at that width), poly_n 5 or 7, winsize <= 17, window
+ * 1..255, <= 6 pyramid levels). Replaces the per-video setup at
  * of:38-62. The gray/pyramid, flow and vote/morphology/output stages run on
  * three internal streams with two batches' rings in flight; `hip_stream`
  * (hipStream_t or NULL) is joined as in dvc_fd_create. Device-pointer steps

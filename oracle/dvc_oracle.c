@@ -509,7 +509,7 @@ struct oc_fd {
 
 oc_fd* oc_fd_create(const dvc_fd_params* p, int use_literal)
 {
-    if (p->width < 1 || p->height < 1 || p->block < 1 || p->block > 1024 || p->ksize < 1 || p->ksize > 63)
+    if (p->width < 1 || p->height < 1 || p->block < 1 || p->block > 1024 || p->ksize < 1 || p->ksize > 1023)
         return NULL;
     if (p->src_width < 0 || p->src_height < 0) return NULL;
     oc_fd* h = (oc_fd*)calloc(1, sizeof(oc_fd));

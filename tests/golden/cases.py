@@ -31,6 +31,10 @@ CASES = {
     "b16_partial": (lambda: clip(200, 120, 12, seed=16, n_objects=3), {"block_size": 16}),
     "b1_min20": (lambda: clip(64, 48, 11, seed=17, n_objects=2), {"block_size": 1, "min_area": 20}),
     "b2_w66": (lambda: clip(66, 50, 11, seed=20, n_objects=2), {"block_size": 2, "min_area": 20}),
+    # the round-4 parameter ranges: blocks beyond 64 (partial edge blocks of 40 / 48 rows)
+    # and dilation kernels beyond 63 (anchor 50 / 63)
+    "s640_b80_k100": (lambda: clip(640, 360, 8, seed=21), {"block_size": 80, "kernel_size": 100}),
+    "s320_b128_k127": (lambda: clip(320, 176, 8, seed=22, n_objects=3), {"block_size": 128, "kernel_size": 127}),
     # cv2.dct raises on an odd side > 1 (fd:122) and the loop ends (fd:140)
     "odd_b5_stops": (lambda: clip(160, 96, 12, seed=18, n_objects=3), {"block_size": 5}),
     "odd_w163_stops": (lambda: clip(163, 96, 14, seed=19, n_objects=3), {}),

@@ -22,6 +22,11 @@ CASES = {
     "of_s133x75_morph5_w3": (lambda: clip(133, 75, 7, seed=14, n_objects=3),                  # odd sides
                              {"morph_kernel": 5, "window_size": 3, "alpha_fraction": 0.4}),
     "of_s330x186_morph4": (lambda: clip(330, 186, 5, seed=15, n_objects=4), {"morph_kernel": 4}),   # 2 levels
+    # the round-4 ranges: vote windows beyond 127 (counts past 127, eviction at 200) and
+    # elements beyond 31
+    "of_noise64_w200": (lambda: np.random.default_rng(16).integers(0, 256, (212, 48, 64, 3), dtype=np.uint8),
+                        {"window_size": 200, "alpha_fraction": 0.9}),
+    "of_s160_morph40": (lambda: clip(160, 96, 6, seed=17, n_objects=3), {"morph_kernel": 40}),
 }
 # cases whose every output pixel is stored in of_golden.npz (the rest: SHA-256 per frame)
 FULL_ARRAYS = ("of_s160_clean", "of_noise64", "of_s162x98", "of_s170x100_morph3")
