@@ -284,11 +284,13 @@ static int check_stop(dvc_fd* h)
                                "implemented, fd:122)", e + 1);
 }
 
-// Can the kernels read these frames in place? (dword rows reaching 3 * gs bytes)
+// Can the kernels read these frames in place? (dword rows reaching 3 * gs
+// bytes; W % 4 == 0 so the last row of a frame span ends at its last quad and a
+// buffer sized to the span is never read past its end)
 static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
-    return h->fmt == DVC_FMT_BGR && !h->resize && pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 &&
-           (n <= 1 || fstride % 4 == 0);
+    return h->fmt == DVC_FMT_BGR && !h->resize && h->p.width % 4 == 0 && pitch % 4 == 0 && pitch >= (size_t)h->ip &&
+           ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
 
 // Can k_front / k_out / k_out_gen read these 4:2:0 surfaces in place (no
@@ -298,8 +300,8 @@ static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_
 static bool direct_yuv(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
     static const int on = [] { const char* e = getenv("DVC_FD_YUV_DIRECT"); return e ? atoi(e) : 1; }();
-    return on && h->fmt != DVC_FMT_BGR && !h->resize && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 &&
-           (n <= 1 || fstride % 4 == 0);
+    return on && h->fmt != DVC_FMT_BGR && !h->resize && h->p.width % 4 == 0 && pitch % 4 == 0 &&
+           ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
 
 static bool host_pinned(const void* p)

@@ -256,19 +256,24 @@ static bool of_pitch_ok(const dvc_of* h, size_t pitch)
 
 // Can the kernels read these BGR device frames in place? Dword rows reaching
 // whole 4-px quads (3 * roundup(W, 4) bytes), aligned base and frame stride;
-// anything else is re-pitched into the slot's staging frames first.
+// anything else is re-pitched into the slot's staging frames first. W % 4 == 0:
+// a frame's last row then ends exactly at its last quad, so a buffer sized to
+// the frame span (pitch * (H - 1) + 3W, what the step checks) is never read
+// past its end.
 static bool of_direct(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
-    return pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
+    return h->p.width % 4 == 0 && pitch % 4 == 0 && pitch >= (size_t)h->ip && ((uintptr_t)p & 3) == 0 &&
+           (n <= 1 || fstride % 4 == 0);
 }
 
 // Can k_of_front0 / k_of_out read these 4:2:0 surfaces in place? Dword luma
-// rows (pitch % 4 == 0, so rows reach whole quads), aligned base and stride.
+// rows (pitch % 4 == 0, so rows reach whole quads), aligned base and stride,
+// W % 4 == 0 (the last luma and chroma rows end at a whole quad's bytes).
 // DVC_OF_YUV_DIRECT=0 forces the staged conversion (A/B).
-static bool of_direct_yuv(const uint8_t* p, size_t pitch, size_t fstride, int n)
+static bool of_direct_yuv(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
     static const int on = [] { const char* e = getenv("DVC_OF_YUV_DIRECT"); return e ? atoi(e) : 1; }();
-    return on && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
+    return on && h->p.width % 4 == 0 && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
 
 // The frames the kernels read for a batch in slot S: the caller's device
@@ -287,7 +292,7 @@ static int of_stage(dvc_of* h, OfSlot& S, const uint8_t* d, int dp, size_t fstri
         *kfs = fstride;
         return DVC_OK;
     }
-    if (h->fmt != DVC_FMT_BGR && of_direct_yuv(d, (size_t)dp, fstride, n)) {
+    if (h->fmt != DVC_FMT_BGR && of_direct_yuv(h, d, (size_t)dp, fstride, n)) {
         const dvc::YuvLayout L = dvc::yuv_layout(d, dp, h->fmt, crows, fstride);
         *sf = dvc::SrcFmt{h->fmt, L.uoff, L.voff, L.cpitch};
         *kd = d;
