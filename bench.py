@@ -213,6 +213,9 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="CPU baseline's multi-core leg: this many feeds on this many host processes (0: every "
                          "available CPU up to the box's CPU share, DVC_CPU_SHARE, default 16)")
+    ap.add_argument("--out-ring", type=int, default=1,
+                    help="output buffer sets written in turn, one per step (an encoder-side ring); 1: every step "
+                         "overwrites the previous step's outputs")
     ap.add_argument("--ktime-seconds", type=float, default=6.0,
                     help="minimum device time of the hipEvent pass that times the dominant kernel")
     ap.add_argument("--runs", type=int, default=5,
@@ -288,14 +291,15 @@ def main():
             seq = torch.empty((P,) + fshape, dtype=torch.uint8, device=dev)
             for j in range(P):
                 seq[j].copy_(torch.from_numpy(ring[idx[j]]))
-            outs = (torch.empty(oshape, dtype=torch.uint8, device=dev),
-                    torch.empty((P, H, W, 3) if of else oshape[0:1] + oshape[1:], dtype=torch.uint8, device=dev))
+            outs = [(torch.empty(oshape, dtype=torch.uint8, device=dev),
+                     torch.empty((P, H, W, 3) if of else oshape[0:1] + oshape[1:], dtype=torch.uint8, device=dev))
+                    for _ in range(max(1, args.out_ring))]
         else:
             alloc = dvc_amd._native.pinned if args.io == "host-pinned" else (lambda shp: np.empty(shp, np.uint8))
             seq = alloc((P,) + fshape)
             for j in range(P):
                 seq[j] = ring[idx[j]]
-            outs = (alloc(oshape), alloc((P, H, W, 3) if of else oshape))
+            outs = [(alloc(oshape), alloc((P, H, W, 3) if of else oshape)) for _ in range(max(1, args.out_ring))]
         first = torch.from_numpy(ring[0]).to(dev) if args.io == "device" else ring[0]
         return seq, outs, first
 
@@ -311,9 +315,13 @@ def main():
         w.prime(inputs[f][2])
         return w
 
+    step_no = [0] * F
+
     def run_feed(w, f, n):
-        seq, (ov, cp), _ = inputs[f]
+        seq, outs, _ = inputs[f]
         for _ in range(n):
+            ov, cp = outs[step_no[f] % len(outs)]   # --out-ring: output sets used in turn, step by step
+            step_no[f] += 1
             if args.per_frame:
                 for j in range(P):
                     w.step(seq[j], ov[j], cp[j])
@@ -461,6 +469,7 @@ def main():
                        "ring_frames": R, "noisy": args.noisy, "in_format": args.in_format,
                        "out_format": "mask + BGR" if of else args.out_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
+                       "output_sets": max(1, args.out_ring),
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),
                        "pipeline_bytes_per_px": pipe,

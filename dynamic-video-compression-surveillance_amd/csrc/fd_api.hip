@@ -490,6 +490,26 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     for (auto sp : {std::make_pair(&h->s_front, level(prio[0])), std::make_pair(&h->s_acc, level(prio[2])),
                     std::make_pair(&h->s_out, level(prio[3]))})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
+    // DVC_CU_SPLIT=k (experiment): the contour filter, accumulate and output /
+    // fix-up streams on k CUs spread evenly over the device, the front on the
+    // others (stream priorities do not apply to CU-masked streams)
+    if (const char* cs = getenv("DVC_CU_SPLIT"); cs && *cs) {
+        int ncu = 256;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+        const int k = std::max(1, std::min(atoi(cs), ncu - 1));
+        std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) {
+            const bool a = (long long)i * k / ncu != (long long)(i + 1) * k / ncu;
+            (a ? ma : mb)[i / 32] |= 1u << (i % 32);
+        }
+        for (hipStream_t* st : {&h->stream, &h->s_acc, &h->s_front, &h->s_out}) (void)hipStreamDestroy(*st);
+        const uint32_t nw = (uint32_t)ma.size() * 32;
+        if ((e = hipExtStreamCreateWithCUMask(&h->stream, nw, ma.data())) != hipSuccess ||
+            (e = hipExtStreamCreateWithCUMask(&h->s_acc, nw, ma.data())) != hipSuccess ||
+            (e = hipExtStreamCreateWithCUMask(&h->s_out, nw, ma.data())) != hipSuccess ||
+            (e = hipExtStreamCreateWithCUMask(&h->s_front, nw, mb.data())) != hipSuccess)
+            return bad(e, "hipExtStreamCreateWithCUMask");
+    }
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame
     for (int k = 0; k < NSLOT; ++k) {
@@ -783,7 +803,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     // place or staged, BGR outputs in dword rows; DVC_FD_FUSED=0 turns it off (A/B)
     static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
     const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && h->B == 4 && sf.fmt == DVC_FMT_BGR &&
-                       !out_i420 && !obytes && (ov || cp);
+                       !out_i420 && !obytes && (ov || cp) && h->SW <= 64;   // k_fix4 scans a row in one wave
     {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
         const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
         S.olo[0] = (uintptr_t)ov;

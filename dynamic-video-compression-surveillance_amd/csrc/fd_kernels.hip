@@ -130,7 +130,7 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 // quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
 // the compressed frame.
 template <int NW, int PF, int FMT, bool OUT>
-__global__ void __launch_bounds__(64 * NW, OUT ? 4 : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
@@ -1207,6 +1207,140 @@ __global__ void __launch_bounds__(256) k_out(BackArgs a, int ntx, int nty)
     }
 }
 
+// The fused front's fix-up (FrontOut, fd_kernels.h), block_size 4, BGR frames
+// in and out: a wave per unit of (frame, RG block rows), grid-stride. One load
+// of the rows' static-block words (lane = (row, word), RG x SW <= 64) finds the
+// 64-block words that hold a full block which is not static; those words are
+// then rewritten two at a time — both words' pixels and acc > 127 fields are
+// loaded before either is computed, so a pair costs one round trip — a lane
+// per block: the compressed frame's YCrCb round trip (fd:115-130) and, where
+// the block has a red pixel, its overlay rows (fd:110-111). A row of a
+// surveillance frame rarely holds more than a few such words.
+struct Fix4 {
+    uint32_t px[4][3];
+    uint16_t rf;
+};
+
+__device__ __forceinline__ void fix4_load(const BackArgs& a, int t, int row, int bx, bool act, Fix4& b)
+{
+    const int bxc = act ? bx : 0, rowc = act ? row : 0;   // inactive lanes load a valid block, unused
+    const uint8_t* f = a.bgr + (size_t)t * a.fstride + (size_t)(rowc * 4) * a.pitch + 12 * (size_t)bxc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)i * a.pitch);
+        b.px[i][0] = v.x;
+        b.px[i][1] = v.y;
+        b.px[i][2] = v.z;
+    }
+    b.rf = a.overlay ? reinterpret_cast<const uint16_t*>(a.rblk)[(size_t)t * a.NBY * a.NBX + (size_t)rowc * a.NBX + bxc]
+                     : (uint16_t)0;
+}
+
+__device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, int bx, const Fix4& b)
+{
+    const size_t o = (size_t)t * a.ostride + (size_t)(row * 4) * a.opitch + 12 * (size_t)bx;
+    if (a.overlay && b.rf) {   // (0, 0, 255) where acc > 127; other blocks keep the speculative copy
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint8_t ob[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool r = (b.rf >> (4 * i + j)) & 1u;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int bi = 3 * j + c;
+                    ob[bi] = r ? (c == 2 ? 255 : 0) : (uint8_t)((b.px[i][bi >> 2] >> (8 * (bi & 3))) & 255);
+                }
+            }
+            uint32_t ow[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
+            store_row<3>(a.overlay + o + (size_t)i * a.opitch, ow, 0);
+        }
+    }
+    if (a.compressed) {   // not static: the YCrCb -> BGR round trip of every pixel
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint8_t ob[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int bb = (b.px[i][(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255;
+                const int gg = (b.px[i][(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255;
+                const int rr = (b.px[i][(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255;
+                const int yv = descale14(bb * 1868 + gg * 9617 + rr * 4899);
+                const int cr = (int)satu8(descale14((rr - yv) * 11682 + (128 << 14))) - 128;
+                const int cb = (int)satu8(descale14((bb - yv) * 9241 + (128 << 14))) - 128;
+                ob[3 * j] = (uint8_t)satu8(yv + descale14(cb * 29049));
+                ob[3 * j + 1] = (uint8_t)satu8(yv + descale14(cb * -5636 + cr * -11698));
+                ob[3 * j + 2] = (uint8_t)satu8(yv + descale14(cr * 22987));
+            }
+            uint32_t cw[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+                cw[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
+            store_row<3>(a.compressed + o + (size_t)i * a.opitch, cw, 0);
+        }
+    }
+}
+
+// position of the r-th (0-based) set bit of m (r < popc(m))
+__device__ __forceinline__ int select_bit(uint64_t m, int r)
+{
+    int base = 0;
+    const int lo = __popc((uint32_t)m);
+    if (r >= lo) { r -= lo; m >>= 32; base = 32; }
+    uint32_t v = (uint32_t)m;
+    const int c16 = __popc(v & 0xffffu);
+    if (r >= c16) { r -= c16; v >>= 16; base += 16; }
+    const int c8 = __popc(v & 0xffu);
+    if (r >= c8) { r -= c8; v >>= 8; base += 8; }
+    for (; r > 0; --r) v &= v - 1;
+    return base + __builtin_ctz(v);
+}
+
+__global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
+{
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    const int SW = a.SW;
+    const int ug = (a.NBY + RG - 1) / RG, total = ug * a.n;
+    const int fullx = a.g.W / 4, fully = a.g.H / 4;   // full blocks (partial edge blocks: k_out_gen)
+    const int lr = lane / SW, lw = lane - lr * SW;     // the lane's (row in the unit, word) in the scan
+    const int nb = min(64, fullx - lw * 64);
+    const uint64_t valid = nb >= 64 ? ~0ull : (nb > 0 ? (1ull << nb) - 1ull : 0ull);
+    for (int u = gw; u < total; u += nw) {   // uniform per wave, no barrier in the loop
+        const int t = u / ug, row0 = (u - t * ug) * RG;
+        const bool ok = lr < RG && row0 + lr < fully;
+        const uint64_t sw = ok ? a.sbits[(size_t)t * a.sstride + (size_t)(row0 + lr) * SW + lw] : ~0ull;
+        const uint64_t ns = ok ? (~sw & valid) : 0ull;   // non-static full blocks of the lane's word
+        // the unit's non-static blocks, compacted onto the lanes: block j of the
+        // unit (in (row, word, bit) order) goes to lane j % 64 of pass j / 64
+        const int cnt = __popcll(ns);
+        const int incl = wave_incl_scan(cnt);
+        const int nblk = __shfl(incl, 63, 64);
+        for (int j0 = 0; j0 < nblk; j0 += 64) {
+            const int j = j0 + lane;
+            const bool act = j < nblk;
+            // source lane: the first s with incl[s] > j (binary search over the lanes)
+            int s = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int probe = s + step - 1;
+                if (__shfl(incl, probe, 64) <= j) s += step;
+            }
+            s = min(s, 63);
+            const int excl = __shfl(incl, s, 64) - __shfl(cnt, s, 64);
+            const uint64_t m = __shfl(ns, s, 64);
+            const int bit = act ? select_bit(m, j - excl) : 0;
+            const int row = row0 + s / SW, bx = (s % SW) * 64 + bit;
+            Fix4 b;
+            fix4_load(a, t, row, bx, act, b);
+            if (act) fix4_store(a, t, row, bx, b);
+        }
+    }
+}
+
 // ------------------------------------------------------------- resize ------
 // cv2.resize(frame, (W, H)) of 8UC3 with INTER_LINEAR (fd:74, fd:91), one lane
 // per output pixel (3 bytes): exact 2x down = OpenCV's INTER_AREA fast path,
@@ -1515,22 +1649,13 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     int chunks = (target / NW + tx * ty / 2) / (tx * ty);
     static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
     if (fo) {
-        // fused outputs (128 VGPRs: 4 workgroups per CU): every workgroup walks
-        // its frames from first to last, so a grid beyond what is resident at
-        // once would run a second round of whole chunks — as many chunks as
-        // fit (1080p: 544 tiles, 1024 resident -> 1); DVC_FUSED_CHUNKS overrides
-        static const int resident = [] {
-            int dev = 0, cus = 256, per = 4;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                cus = 256;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_front<4, 1, DVC_FMT_BGR, true>, 256, 0) !=
-                    hipSuccess || per < 1)
-                per = 4;
-            return per * cus;
-        }();
+        // fused outputs (128 VGPRs: 4 workgroups per CU): chunks of ~48 frames
+        // (1080p x 383: 8 chunks, 4352 workgroups; measured alone 373 k / 514 k /
+        // 534 k Mpx/s at 1 / 4 / 8 chunks — a warm-up frame per chunk is 2 % more
+        // reads, more workgroups in flight hide the per-frame barriers);
+        // DVC_FUSED_CHUNKS overrides
         static const int fc = [] { const char* e = getenv("DVC_FUSED_CHUNKS"); return e ? atoi(e) : 0; }();
-        chunks = fc > 0 ? fc : resident / (tx * ty);
+        chunks = fc > 0 ? fc : std::max(1, n / 48);
     }
     chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;
@@ -1541,8 +1666,12 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     const FrontOut none{};
     if constexpr (NW == 4) {
         if (fo) {
-            hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
-                               gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+            if (pf == 2)
+                hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n,
+                                   chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+            else
+                hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n,
+                                   chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             return;
         }
     }
@@ -1729,7 +1858,17 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
     const int f = a.sf.fmt;
     if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR in and out, dword rows)
         if (B != 4 || f != DVC_FMT_BGR || a.out_i420 || a.obytes) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+        static const int fwgs = [] {   // DVC_FIX_WGS: k_fix4 workgroups (default 6 per CU: all resident at 79 VGPRs)
+            if (const char* e = getenv("DVC_FIX_WGS")) return std::max(1, atoi(e));
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                cus = 256;
+            return 6 * cus;
+        }();
+        if (a.SW > 64) return hipErrorInvalidValue;   // rows of <= 64 words (W <= 16384 px): the scan's lanes
+        const int RG = std::max(1, 64 / a.SW), units = (a.NBY + RG - 1) / RG * a.n;
+        hipLaunchKernelGGL(k_fix4, dim3(std::max(1, std::min(fwgs, (units + 3) / 4))), dim3(256), 0, s, a, RG);
     }
     else if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);

@@ -245,7 +245,7 @@ def test_batch_device_matches_steps(gpu_lib):
 def test_errors(gpu_lib):
     from dvc_amd._native import DvcError
     with pytest.raises(DvcError):
-        gpu_lib.FDWorker(640, 360, block_size=65)   # the GPU path implements block sizes 1..64
+        gpu_lib.FDWorker(640, 360, block_size=129)  # the GPU path implements block sizes 1..128
     with pytest.raises(DvcError):
         gpu_lib.FDWorker(8, 360)                    # frames of at least 16 x 16
     w = gpu_lib.FDWorker(640, 360)

@@ -188,7 +188,7 @@ def test_of_compress_arbitrary_mask(gpu_lib, oracle_lib, density):
 def test_of_rejects_unsupported(gpu_lib):
     with pytest.raises(gpu_lib._native.DvcError):
         gpu_lib.OFWorker(7, 360)            # frames of at least 8 x 8
-    for k in (0, 32):                       # morph_kernel 1..31
+    for k in (0, 65):                       # morph_kernel 1..64
         with pytest.raises(gpu_lib._native.DvcError):
             gpu_lib.OFWorker(640, 360, morph_kernel=k)
     w = gpu_lib.OFWorker(160, 96)

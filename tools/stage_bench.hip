@@ -2,7 +2,9 @@
 // kernels of fd_kernels.hip stage by stage, each stage alone on the device
 // (synchronised between stages), over one batch of n synthetic frames, so a
 // rocprofv3 kernel trace shows every kernel's isolated duration.
-//   stage_bench W H n reps frames.raw   (frames.raw: n+1 packed BGR frames)
+//   stage_bench W H n reps frames.raw [fused]   (frames.raw: n+1 packed BGR frames;
+//   fused = 1: the fused front's speculative outputs + k_fix4, as the handle runs
+//   block_size 4 with BGR frames)
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -29,6 +31,7 @@ int main(int argc, char** argv)
         return 2;
     }
     const int W = std::atoi(argv[1]), H = std::atoi(argv[2]), n = std::atoi(argv[3]), reps = std::atoi(argv[4]);
+    const bool fused = argc > 6 && std::atoi(argv[6]) != 0;
     const size_t F = (size_t)3 * W * H, N = (size_t)W * H;
     std::vector<uint8_t> host(F * (n + 1));
     FILE* fp = std::fopen(argv[5], "rb");
@@ -60,6 +63,7 @@ int main(int argc, char** argv)
     for (int i = 0; i < dvc::CclBufs::NARR; ++i) CK(hipMalloc(ptrs[i], sz[i]));
     CK(hipMemset(c.gpar, 0, sz[6]));
     c.stats = stats;
+    CK(hipMalloc(&c.kocc, (size_t)H * n));   // sparse kept rows, as the handle runs it
     const int B = 4, NBX = (W + B - 1) / B, NBY = (H + B - 1) / B, SW = (NBX + 63) / 64, gs = (W + 3) & ~3;
     uint64_t *dblk, *rblk, *sbits;
     CK(hipMalloc(&dblk, 2 * (size_t)NBX * NBY * n));
@@ -86,6 +90,8 @@ int main(int argc, char** argv)
     a.opitch = 3 * W;
     a.ostride = F;
     a.kbits = c.kbits;
+    a.kocc = c.kocc;
+    CK(hipMalloc(&a.docc, (size_t)NBY * n));
     a.dblk = dblk;
     a.rblk = rblk;
     a.sbits = sbits;
@@ -114,15 +120,17 @@ int main(int argc, char** argv)
         auto t0 = std::chrono::steady_clock::now();
         // rep 0 starts from the 25x25-blurred prime gray (a near-full first mask);
         // later reps continue from the previous rep's last gray like a feed would
+        dvc::FrontOut fo{ov, cp, 3 * W, F, 100.f, 1.0 / 100.0, a.M};
         CK(dvc::launch_front(frames + F, 3 * W, F, dvc::SrcFmt{0, 0, 0, 0}, n, (r & 1) ? gray1 : gray0, (r & 1) ? gray0 : gray1, gs, c.mbits, g,
-                             0, nullptr));
+                             0, nullptr, fused ? &fo : nullptr));
         CK(hipDeviceSynchronize());
         auto t1 = std::chrono::steady_clock::now();
         CK(dvc::launch_ccl(c, g, n, 1000, nullptr));
         CK(hipDeviceSynchronize());
         auto t2 = std::chrono::steady_clock::now();
         CK(dvc::launch_accumulate(a, nullptr));
-        CK(dvc::launch_out(a, nullptr));
+        CK(hipDeviceSynchronize());
+        CK(dvc::launch_out(a, nullptr, fused));
         CK(hipDeviceSynchronize());
         auto t3 = std::chrono::steady_clock::now();
         if (r > 0) {
