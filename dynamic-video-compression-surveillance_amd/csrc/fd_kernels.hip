@@ -135,13 +135,17 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
 {
-    static_assert(!OUT || (NW == 4 && FMT == DVC_FMT_BGR), "fused outputs: 16-row tiles of BGR frames");
+    static_assert(!OUT || ((NW == 4 || NW == 8) && FMT == DVC_FMT_BGR), "fused outputs: 16- or 32-row tiles of BGR frames");
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // LDS row of this wave's j-th loaded row, and tile row of its i-th output row
-    auto lrow = [&](int j) { return OUT ? (j < 4 ? 2 + 4 * wave + j : (wave < 2 ? wave : 16 + wave)) : wave + NW * j; };
+    // (OUT: the 4 halo rows 0, 1, FT_H + 2, FT_H + 3 go to waves 0..3; a wave
+    // past them has no 5th row: FT_R, never stored)
+    auto lrow = [&](int j) {
+        return OUT ? (j < 4 ? 2 + 4 * wave + j : (wave < 2 ? wave : (wave < 4 ? FT_H + wave : FT_R))) : wave + NW * j;
+    };
     auto orow = [&](int i) { return OUT ? 4 * wave + i : wave + NW * i; };
     // XCD bands: blocks b, b+8, .. share an XCD (and its L2); the bijective remap
     // below deals each such group a contiguous run of (chunk, tile row, tile)
@@ -1664,13 +1668,16 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     static const int pf = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 1; }();
     const dim3 grid(tx, ty, chunks), block(64 * NW);
     const FrontOut none{};
-    if constexpr (NW == 4) {
+    if constexpr (NW == 4 || NW == 8) {
         if (fo) {
-            if (pf == 2)
-                hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n,
+            // DVC_FRONT_LDS=<bytes> (experiment): unused dynamic LDS per workgroup, to
+            // cap the fused front's workgroups per CU and leave room to the others
+            static const size_t pad = [] { const char* e = getenv("DVC_FRONT_LDS"); return e ? (size_t)atol(e) : 0; }();
+            if (pf == 2 && NW == 4)
+                hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             else
-                hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true>), grid, block, 0, s, bgr, pitch, fstride, sf, n,
+                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             return;
         }
@@ -1697,7 +1704,7 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const Src
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
     if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
-    else if (nw == 8 && !fo) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
+    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     return hipGetLastError();
 }
