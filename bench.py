@@ -213,9 +213,10 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0,
                     help="CPU baseline's multi-core leg: this many feeds on this many host processes (0: every "
                          "available CPU up to the box's CPU share, DVC_CPU_SHARE, default 16)")
-    ap.add_argument("--out-ring", type=int, default=1,
-                    help="output buffer sets written in turn, one per step (an encoder-side ring); 1: every step "
-                         "overwrites the previous step's outputs")
+    ap.add_argument("--out-ring", type=int, default=2,
+                    help="output buffer sets written in turn, one per step: the encoder side reads one set while "
+                         "the next step writes the other (default 2); 1: every step overwrites the previous step's "
+                         "outputs, so a fused-front batch waits for the fix-up of the batch two before it")
     ap.add_argument("--ktime-seconds", type=float, default=6.0,
                     help="minimum device time of the hipEvent pass that times the dominant kernel")
     ap.add_argument("--runs", type=int, default=5,

@@ -174,8 +174,9 @@ def lib() -> ctypes.CDLL:
     L.dvc_fd_get_stats.argtypes = [vp, ctypes.POINTER(FdStats)]
     L.dvc_fd_read_plane.argtypes = [vp, ctypes.c_int, u8p]
     L.dvc_fd_ktime.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    L.dvc_fd_ktime_kernel.argtypes = [vp]
-    L.dvc_fd_ktime_kernel.restype = ctypes.c_int
+    if hasattr(L, "dvc_fd_ktime_kernel"):   # (an older build under DVC_LIB_PATH lacks it)
+        L.dvc_fd_ktime_kernel.argtypes = [vp]
+        L.dvc_fd_ktime_kernel.restype = ctypes.c_int
     L.dvc_fd_destroy.argtypes = [vp]
     L.dvc_fd_destroy.restype = None
     L.dvc_gaussian_taps_q8.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint16)]
@@ -231,7 +232,7 @@ def lib() -> ctypes.CDLL:
                  "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime", "dvc_gaussian_taps_q8",
                  "dvc_contour_filter", "dvc_fd_step_batch"):
         getattr(L, name).restype = ctypes.c_int
-    if L.dvc_abi_version() != ABI_VERSION:
+    if L.dvc_abi_version() != ABI_VERSION and not os.environ.get("DVC_LIB_PATH"):   # A/B of older builds
         raise ImportError("libdvc_hip.so ABI version mismatch")
     _lib = L
     return L

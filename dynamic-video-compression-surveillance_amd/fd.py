@@ -204,6 +204,8 @@ class FDWorker:
     def ktime_kernel(self) -> str:
         """Which kernel ktime() timed in the last batch: "k_front_fused" (the fused
         front with the speculative outputs) or "k_out"."""
+        if not hasattr(self._lib, "dvc_fd_ktime_kernel"):   # an older build (DVC_LIB_PATH A/B)
+            return "k_out"
         k = self._lib.dvc_fd_ktime_kernel(self._h)
         if k < 0:
             N.check(k)
