@@ -2,10 +2,10 @@
 # GPU box: the HEAD evidence set kept under profiles/ — bench lines (FD 1080p,
 # 4K, noisy, NV12 input; OF 1080p, NV12 input), kernel-trace + PMC profiles of
 # the FD and OF headline workloads, the OF SQ counters, the drop-in drivers.
-#   tools/refresh_r3.sh <tag>      (outputs under gpurun_out/<tag>/)
+#   tools/refresh_r4.sh <tag>      (outputs under gpurun_out/<tag>/)
 set -e
 cd "$(dirname "$0")/.."
-TAG=${1:-r3}
+TAG=${1:-r4}
 O=gpurun_out/$TAG
 mkdir -p $O
 b() { local name=$1; shift; timeout -k 10 400 python3 -u bench.py "$@" > $O/bench_$name.json 2> $O/bench_$name.err; tail -c 300 $O/bench_$name.json; echo; }
