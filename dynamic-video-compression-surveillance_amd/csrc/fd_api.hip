@@ -902,6 +902,10 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     {
         const float z = std::rint(std::fmaf(0.0f, h->p.alpha, std::fmaf(0.0f, h->p.beta, h->p.gamma)));
         a.acc0_fixed = z < 0.5f && z > -0.5f;  // saturate_cast<uchar>(0) == 0 (NaN/negatives excluded)
+        const float dil1 = std::fmaf(255.0f, h->p.beta, h->p.gamma);
+        static const bool acc_general = getenv("DVC_ACC_GENERAL") != nullptr;  // A/B: the general form always
+        a.acc_fast = dvc::acc_fast_ok(h->p.alpha, h->p.beta, h->p.gamma) && !acc_general;
+        std::memcpy(&a.dil1_bits, &dil1, 4);
     }
     a.M = h->M;
     a.Mtab = h->Mtab;

@@ -140,6 +140,8 @@ struct BackArgs {
     float alpha, beta, gamma, quant;
     double qinv;            // RN53(1 / (double)quant): the quantiser division as a product (div_rn)
     int acc0_fixed;         // addWeighted(acc 0, dilated 0) == 0: zero blocks stay zero
+    int acc_fast;           // k_acc's short form holds (acc_fast_ok): dil0 == +0, no clamp can bind
+    uint32_t dil1_bits;     // bits of fmaf(255, beta, gamma), the dilated-pixel addend
     DctMat M;               // fast B x B basis (kernargs)
     const float* Mtab;      // generic bases in device memory: M_B (B*B) | M_{W%B} | M_{H%B}
     unsigned long long* stats;
@@ -194,6 +196,20 @@ size_t ccl_max_lds(const RowGeom& g);   // dvc_fd_create refuses frames wider th
 hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_area2, hipStream_t s);
 // k_dilate then k_acc (the accumulated-mask recurrence: batches in order)
 hipError_t launch_accumulate(const BackArgs& a, hipStream_t s);
+// k_acc's short form computes fmaf(acc, alpha, D) with D = +0 or fmaf(255, beta,
+// gamma) and drops the [0, 255] clamp. Exact when fmaf(0, beta, gamma) is +0
+// (the dilated-0 addend; D is then a sign-mask AND of the dil-1 bits) and the
+// clamp cannot bind: fmaf and round-to-nearest-even are monotone in acc and D,
+// so with alpha >= 0 and D >= 0 every result lies between rint(+0) = 0 and
+// rint(fmaf(255, alpha, D1)) <= 255 (NaN fails every comparison below).
+inline bool acc_fast_ok(float alpha, float beta, float gamma)
+{
+    const float d0 = __builtin_fmaf(0.0f, beta, gamma), d1 = __builtin_fmaf(255.0f, beta, gamma);
+    uint32_t d0b;
+    __builtin_memcpy(&d0b, &d0, 4);
+    return d0b == 0 && alpha >= 0.0f && alpha <= 1.0f && d1 >= 0.0f && d1 <= 255.0f &&
+           __builtin_rintf(__builtin_fmaf(255.0f, alpha, d1)) <= 255.0f;
+}
 // k_out (overlay + compressed frames; no recurrence) and k_out_gen for the
 // generic layout / partial edge blocks (always launched: it also detects the
 // odd-size DCT stop and counts generic static blocks). fix: the fused front

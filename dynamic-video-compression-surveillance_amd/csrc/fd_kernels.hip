@@ -823,33 +823,69 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
     // read; a block row whose whole window is empty writes no fields, only
     // docc = 0, and k_acc then reads none either
     const uint8_t* ko = a.kocc ? a.kocc + (size_t)t * H : nullptr;
+    // Loads are unconditional from clamped addresses and unrolled, so several
+    // are in flight at once (a load behind a per-row test waits out the one
+    // before it). Window rows kept (in the image and, sparse, with kept bits):
+    // bit r of kmask for windows of <= 64 rows, ko re-read past that.
+    const int R = B + k - 1;
+    auto in_img = [&](int r) { const int y = y0 - an + r; return y >= 0 && y < H; };
+    auto row_of = [&](int r) { return min(max(y0 - an + r, 0), H - 1); };
+    uint64_t kmask = 0;
     if (ko) {
         int any = 0;
-        for (int r = 0; r < B + k - 1; ++r) {
-            const int y = y0 - an + r;
-            if (y >= 0 && y < H) any |= ko[y];
+#pragma unroll 8
+        for (int r = 0; r < R; ++r) {
+            const int kp = (int)in_img(r) & (int)(ko[row_of(r)] != 0);
+            any |= kp;
+            kmask |= (uint64_t)kp << (r & 63);
         }
         if (wi == 0) a.docc[(size_t)by * a.n + t] = (uint8_t)any;
         if (!any && !(a.dbg_dil && t == a.n - 1)) return;
+    } else {
+        for (int r = 0; r < min(R, 64); ++r) kmask |= (uint64_t)in_img(r) << r;
     }
     // pixels past W (the last word) are not pixels: their dilated bits stay 0
     const uint64_t vmask = (wi == WW - 1 && (W & 63)) ? (1ull << (W & 63)) - 1ull : ~0ull;
+    const int wl = max(wi - 1, 0), wr = min(wi + 1, WW - 1);
     uint64_t out[B];
 #pragma unroll
     for (int i = 0; i < B; ++i) out[i] = 0;
-    for (int r = 0; r < B + k - 1; ++r) {
-        const int y = y0 - an + r;
-        if (y < 0 || y >= H || (ko && !ko[y])) continue;
-        const uint64_t* row = kb + (size_t)y * WW;
-        const uint64_t c = row[wi], pv = wi > 0 ? row[wi - 1] : 0ull, nv = wi + 1 < WW ? row[wi + 1] : 0ull;
-        uint64_t o = c;
-        for (int off = 1; off <= k - 1 - an; ++off) o |= (c >> off) | (nv << (64 - off));
-        for (int off = 1; off <= an; ++off) o |= (c << off) | (pv >> (64 - off));
-        o &= vmask;
+    // rows four at a time: the 12 loads first (rows not kept read row 0 and
+    // are discarded), then the shifts
+    auto rows = [&](auto big) {   // big: windows past 64 rows test ko per row
+        for (int r0 = 0; r0 < R; r0 += 4) {
+            uint64_t c[4], pv[4], nv[4];
 #pragma unroll
-        for (int i = 0; i < B; ++i)
-            if (r - i >= 0 && r - i < k) out[i] |= o;
-    }
+            for (int u = 0; u < 4; ++u) {
+                const int r = r0 + u;
+                bool keep;
+                if constexpr (decltype(big)::value) keep = r < R && in_img(r) && (!ko || ko[row_of(r)]);
+                else keep = r < R && ((kmask >> r) & 1) != 0;
+                const uint64_t* row = kb + (keep ? (size_t)row_of(r) * WW : 0);
+                const uint64_t c0 = row[wi], p0 = row[wl], n0 = row[wr];
+                // the masks pass through an empty asm so that the compiler
+                // cannot turn "keep ? load : 0" back into a branch around the load
+                uint32_t mc = keep ? ~0u : 0u, mp = keep && wi > 0 ? ~0u : 0u, mn = keep && wi + 1 < WW ? ~0u : 0u;
+                asm("" : "+v"(mc), "+v"(mp), "+v"(mn));
+                c[u] = c0 & (((uint64_t)mc << 32) | mc);
+                pv[u] = p0 & (((uint64_t)mp << 32) | mp);
+                nv[u] = n0 & (((uint64_t)mn << 32) | mn);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = r0 + u;
+                uint64_t o = c[u];
+                for (int off = 1; off <= k - 1 - an; ++off) o |= (c[u] >> off) | (nv[u] << (64 - off));
+                for (int off = 1; off <= an; ++off) o |= (c[u] << off) | (pv[u] >> (64 - off));
+                o &= vmask;
+#pragma unroll
+                for (int i = 0; i < B; ++i)
+                    if (r - i >= 0 && r - i < k) out[i] |= o;
+            }
+        }
+    };
+    if (R <= 64) rows(std::false_type{});
+    else rows(std::true_type{});
 #pragma unroll
     for (int i = 0; i < B; ++i)   // rows past H (a partial last block row) are not pixels
         if (y0 + i >= H) out[i] = 0;
@@ -870,10 +906,30 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
     }
 }
 
+// Bit 7 of each byte of w[0..3] (4 pixels a word) as 16 bits, pixel j of word k
+// at bit 4k + j. Packed 16-bit multiplies gather bits without carries (every
+// product's set bits land on distinct positions) and byte permutes keep the
+// bytes holding them: 11 VALU for 16 pixels instead of ~45 shifts and masks.
+__device__ __forceinline__ uint32_t hibits16(const uint32_t (&w)[4])
+{
+    auto pm = [](uint32_t x, unsigned short k) { return as_u32(as_u16x2(x) * (u16x2)k); };
+    uint32_t y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[k] = pm(w[k] & 0x80808080u, 0x81);   // half: bits 7, 15 -> 14, 15
+    // bytes 1, 3 of two words: the first word's pixels at 6, 7, 14, 15, the second's at 22, 23, 30, 31
+    const uint32_t z01 = __builtin_amdgcn_perm(y[1], y[0], 0x07050301u);
+    const uint32_t z23 = __builtin_amdgcn_perm(y[3], y[2], 0x07050301u);
+    // half: bits 6, 7, 14, 15 -> 12..15; bytes 1, 3 again: word k's nibble at 8k + 4
+    const uint32_t v = __builtin_amdgcn_perm(pm(z23, 0x41), pm(z01, 0x41), 0x07050301u);
+    // half: nibbles at 4, 12 -> 8..15 (bytes 1, 3)
+    return __builtin_amdgcn_perm(0u, pm(v, 0x11), 0x04040301u);
+}
+
 // One lane per BxB block (64 blocks across per wave, one block row), frames in
 // order with the block's acc bytes in registers; the block fields of 8 frames
-// are loaded one chunk ahead.
-template <int B>
+// are loaded one chunk ahead. FAST (acc_fast_ok): the dilated addend is a
+// sign-mask AND, the multiply-adds run as packed pairs and the clamp is gone.
+template <int B, bool FAST>
 __global__ void __launch_bounds__(64) k_acc(BackArgs a)
 {
     typedef typename BlkT<B>::T BT;
@@ -897,13 +953,31 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
     constexpr int U = 8;
     BT dA[U], dB[U];
     // docc (uniform over the workgroup's block row): frames whose block row has
-    // no dilated bit load no field
+    // no dilated bit take a zero field. Read once up front as a frame bit mask
+    // in LDS, so that the field loads below are unconditional and never wait:
+    // a load behind a per-frame docc test drained vmcnt to 0 before each one
+    // (two memory round trips a frame, the kernel's whole time).
+    __shared__ unsigned long long dmask[DVC_MAX_BATCH / 64];
     const uint8_t* dc = a.docc ? a.docc + (size_t)by * a.n : nullptr;
-    auto load_chunk = [&](int t0, BT (&dst)[U]) {
+    if (dc) {
+        uint8_t v[DVC_MAX_BATCH / 64];
+#pragma unroll
+        for (int c = 0; c < DVC_MAX_BATCH / 64; ++c) v[c] = dc[min(c * 64 + lane, a.n - 1)];
+#pragma unroll
+        for (int c = 0; c < DVC_MAX_BATCH / 64; ++c) {
+            const unsigned long long m = __ballot(c * 64 + lane < a.n && v[c] != 0);
+            if (lane == 0) dmask[c] = m;
+        }
+        __syncthreads();
+    }
+    auto load_chunk = [&](int t0, BT (&dst)[U]) {   // t0 % 8 == 0: one mask word
+        const unsigned long long m = dc ? dmask[min(t0, DVC_MAX_BATCH - 1) >> 6] >> (t0 & 63) : ~0ull;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int tt = min(t0 + u, a.n - 1);   // clamped: the last frames reload
-            dst[u] = (!dc || dc[tt]) ? db[(size_t)tt * NB + blk] : (BT)0;
+            const bool on = (m >> u) & 1u;
+            const BT v = db[on ? (size_t)tt * NB + blk : blk];   // off: frame 0's field, discarded
+            dst[u] = on ? v : (BT)0;
         }
     };
     unsigned long long nstatic = 0;
@@ -917,7 +991,33 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
         // addWeighted (fd:107); an all-zero block with no dilated pixel stays all
         // zero when addWeighted(0, 0) = 0 (a.acc0_fixed), skipping the float math
         bool zero = true;
-        if (!(a.acc0_fixed && d == 0 && aor == 0)) {
+        if (FAST && !(d == 0 && aor == 0)) {   // acc_fast_ok implies acc0_fixed
+            const f32x2 al = (f32x2)a.alpha;
+            uint32_t nor = 0;
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                const uint32_t dw = (uint32_t)((d >> (B * i)) & ROWM);
+#pragma unroll
+                for (int q = 0; q < B / 4; ++q) {
+                    const uint32_t av = acv[i][q];
+                    float dv[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)   // D = dil bit ? dil1 : +0
+                        dv[j] = __builtin_bit_cast(float, (uint32_t)((int32_t)(dw << (31 - 4 * q - j)) >> 31) & a.dil1_bits);
+                    const f32x2 t01 = __builtin_elementwise_fma(
+                        (f32x2){(float)(av & 255), (float)((av >> 8) & 255)}, al, (f32x2){dv[0], dv[1]});
+                    const f32x2 t23 = __builtin_elementwise_fma(
+                        (f32x2){(float)((av >> 16) & 255), (float)(av >> 24)}, al, (f32x2){dv[2], dv[3]});
+                    uint32_t nv = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_rintf(t01.x), 0u, 0u);
+                    nv = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_rintf(t01.y), 1u, nv);
+                    nv = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_rintf(t23.x), 2u, nv);
+                    nv = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_rintf(t23.y), 3u, nv);
+                    acv[i][q] = nv;
+                    nor |= nv;
+                }
+            }
+            zero = nor == 0;
+        } else if (!FAST && !(a.acc0_fixed && d == 0 && aor == 0)) {
 #pragma unroll
             for (int i = 0; i < B; ++i) {
                 const uint32_t dw = (uint32_t)((d >> (B * i)) & ROWM);
@@ -941,15 +1041,16 @@ __global__ void __launch_bounds__(64) k_acc(BackArgs a)
             }
         }
         // bits out: acc > 127 per pixel (bit 7 of each byte), all-zero per block
+        // (word k = B/4 * i + q holds bits 4k .. 4k + 3 of the field)
         BT r = 0;
 #pragma unroll
-        for (int i = 0; i < B; ++i)
-#pragma unroll
-            for (int q = 0; q < B / 4; ++q) {
-                const uint32_t hb = acv[i][q] & 0x80808080u;
-                const uint32_t m = ((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u);
-                r |= (BT)((BT)m << (B * i + 4 * q));
-            }
+        for (int g = 0; g < B * B / 16; ++g) {
+            const uint32_t w[4] = {acv[(4 * g) / (B / 4)][(4 * g) % (B / 4)],
+                                   acv[(4 * g + 1) / (B / 4)][(4 * g + 1) % (B / 4)],
+                                   acv[(4 * g + 2) / (B / 4)][(4 * g + 2) % (B / 4)],
+                                   acv[(4 * g + 3) / (B / 4)][(4 * g + 3) % (B / 4)]};
+            r |= (BT)((BT)hibits16(w) << (16 * g));
+        }
         // a static block (acc all zero) has no acc > 127 bit: its field is not
         // written, k_out / k_out_gen take it as zero from sbits
         if (active && !zero) rb[(size_t)t * NB + blk] = r;
@@ -1813,7 +1914,10 @@ template <int B>
 static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(k_dilate<B>, dim3((a.g.WW * a.NBY + 255) / 256, a.n), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_acc<B>, dim3(a.SW, a.NBY), dim3(64), 0, s, a);
+    if (a.acc_fast)
+        hipLaunchKernelGGL((k_acc<B, true>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_acc<B, false>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
