@@ -121,7 +121,7 @@ struct Slot {
     bool recorded = false;  // the events hold a batch that the next user of the slot must wait for
     // the output bytes its batch writes ([lo, hi) of overlay and compressed; empty
     // when not requested): a fused front writes outputs before the previous
-    // batches' k_fix have run, so it waits for those that write the same bytes
+    // batches' k_fix4 have run, so it waits for those that write the same bytes
     uintptr_t olo[2] = {0, 0}, ohi[2] = {0, 0};
 };
 
@@ -769,10 +769,12 @@ int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
 
 // Enqueue one batch i of n <= max_batch frames, slot S = i % 3 (j = i - 3 =
 // the slot's previous batch):
-//   s_front:         [wait ccl(j) (+ out(j) when staging)]  stage, front(i) -> ev_front   (S.mbits free)
+//   s_front:         [wait ccl(j) (+ out(j) when staging or fused; fused: also
+//                    out(i-1), out(i-2) where their output bytes overlap)]
+//                    stage, front(i) (fused: + speculative outputs) -> ev_front   (S.mbits free)
 //   stream:          [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
 //   s_acc:           [wait ev_ccl, out(j)]    dilate + accumulate(i) -> ev_acc (S bits free)
-//   s_out:           [wait ev_acc]            k_out(i) -> ev_out
+//   s_out:           [wait ev_acc]            k_out(i), or k_out_gen + k_fix4(i) when fused -> ev_out
 // so front(i+2), the contour filter of i+1, the accumulation of i and the
 // output of i-1 can all be in flight; the two recurrences (previous gray,
 // accumulated mask) are serial, each on its own stream.
@@ -813,9 +815,9 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     }
     dvc::FrontOut fo{};
     if (fused) {
-        // the speculative stores must not land before an earlier batch's k_fix
+        // the speculative stores must not land before an earlier batch's k_fix4
         // rewrites the same bytes: wait for the slot's previous batch (so every
-        // k_fix up to batch i-3 is done, s_out being in order) and for batches
+        // k_fix4 up to batch i-3 is done, s_out being in order) and for batches
         // i-1, i-2 where their outputs overlap this one's
         if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
         for (int k = 1; k < NSLOT; ++k) {

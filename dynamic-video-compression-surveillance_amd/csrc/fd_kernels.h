@@ -160,7 +160,7 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
 // its 4x4 blocks in registers it writes every full block as if it were static —
 // overlay = the frame (no acc > 127 pixel can lie in a block whose acc is all
 // zero, fd:110-111) and compressed = (Y', Y', Y') of the block's quantised DCT
-// (fd:117-130) — and k_fix (k_out<.., FIX>) later rewrites only the blocks the
+// (fd:117-130) — and k_fix4 later rewrites only the blocks the
 // accumulated mask makes non-static (their YCrCb round trip, and the red
 // overlay where acc > 127). Every output byte ends equal to k_out's.
 struct FrontOut {

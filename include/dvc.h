@@ -81,7 +81,7 @@ extern "C" {
 #define DVC_FLAG_FD_UNFUSED  0x40u /* FD: write the outputs in one k_out pass after
                                      the accumulated mask instead of the fused
                                      front's speculative static-block outputs +
-                                     k_fix (same bytes; the fused form reads each
+                                     k_fix4 (same bytes; the fused form reads each
                                      frame from HBM once instead of twice. It
                                      applies to block_size 4, BGR frames in and
                                      out, 4-byte aligned output rows; the
