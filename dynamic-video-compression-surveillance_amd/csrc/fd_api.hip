@@ -801,11 +801,12 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     const int opitch = 3 * h->p.width;
     const int obytes = (opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
     const bool out_i420 = h->p.flags & DVC_FLAG_OUT_I420;
-    // fused front (fd_kernels.h FrontOut): block_size 4, BGR frames read in
-    // place or staged, BGR outputs in dword rows; DVC_FD_FUSED=0 turns it off (A/B)
+    // fused front (fd_kernels.h FrontOut): block_size 4, BGR frames or 4:2:0
+    // surfaces read in place (or staged), BGR outputs in dword rows;
+    // DVC_FD_FUSED=0 turns it off (A/B)
     static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
-    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && h->B == 4 && sf.fmt == DVC_FMT_BGR &&
-                       !out_i420 && !obytes && (ov || cp) && h->SW <= 64;   // k_fix4 scans a row in one wave
+    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && h->B == 4 && !out_i420 && !obytes &&
+                       (ov || cp) && h->SW <= 64;   // k_fix4 scans a row in one wave
     {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
         const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
         S.olo[0] = (uintptr_t)ov;

@@ -155,7 +155,7 @@ struct BackArgs {
 hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32_t* tmp32, uint8_t* out,
                         int W, int H, int gs, const GaussTaps& k, hipStream_t s);
 
-// Speculative outputs of the fused front (block_size 4, BGR frames in and out,
+// Speculative outputs of the fused front (block_size 4, BGR outputs; BGR frames or 4:2:0 surfaces read in place;
 // dword-aligned output rows). A frame is read from HBM once: while k_front has
 // its 4x4 blocks in registers it writes every full block as if it were static —
 // overlay = the frame (no acc > 127 pixel can lie in a block whose acc is all

@@ -122,11 +122,12 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
     }
 }
 
-// OUT (fused speculative outputs, FrontOut in fd_kernels.h; NW = 4, BGR): the
+// OUT (fused speculative outputs, FrontOut in fd_kernels.h; NW = 4 or 8): the
 // rows are dealt by block row instead — wave w loads and owns tile rows
 // 4w..4w+3, so each lane holds one 4x4 block of the frame, plus one halo row
 // (LDS rows 0, 1, 18, 19 for waves 0..3) — and the block's pixels go out as
-// the overlay straight from the registers they were loaded into, its gray
+// the overlay straight from the registers they were loaded into (4:2:0
+// surfaces: converted to BGR once, for the overlay and the gray), its gray
 // quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
 // the compressed frame.
 template <int NW, int PF, int FMT, bool OUT>
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
 {
-    static_assert(!OUT || ((NW == 4 || NW == 8) && FMT == DVC_FMT_BGR), "fused outputs: 16- or 32-row tiles of BGR frames");
+    static_assert(!OUT || NW == 4 || NW == 8, "fused outputs: 16- or 32-row tiles");
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
@@ -253,8 +254,24 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
     const bool full_blk = OUT && x + 4 <= W && y0 + 4 * wave + 4 <= H;
     const size_t orow0 = (size_t)(y0 + 4 * wave) * fo.opitch + 3 * (size_t)x;
     auto frame = [&](Quads& qs, int t) {
+        // OUT: the block's 4 rows as BGR (4:2:0 surfaces converted once, for
+        // both the gray and the overlay); other rows straight to gray
+        uint32_t cb[4][3];
+        if constexpr (OUT) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j)
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (YUV) {
+                    quad_bgr<FMT>(qs.v0[j], qs.v1[j], qs.v2[j], cb[j]);
+                } else {
+                    cb[j][0] = qs.v0[j];
+                    cb[j][1] = qs.v1[j];
+                    cb[j][2] = qs.v2[j];
+                }
+                sg[lrow(j)][lane + 1] = gray4_dot(cb[j][0], cb[j][1], cb[j][2]);
+            }
+        }
+#pragma unroll
+        for (int j = OUT ? 4 : 0; j < NR; ++j)
             if (NR * NW == FT_R || lrow(j) < FT_R)
                 sg[lrow(j)][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
         if constexpr (OUT) {
@@ -265,9 +282,9 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     uint32_t* r = reinterpret_cast<uint32_t*>(o + (size_t)j * fo.opitch);
-                    __builtin_nontemporal_store(qs.v0[j], r);
-                    __builtin_nontemporal_store(qs.v1[j], r + 1);
-                    __builtin_nontemporal_store(qs.v2[j], r + 2);
+                    __builtin_nontemporal_store(cb[j][0], r);
+                    __builtin_nontemporal_store(cb[j][1], r + 1);
+                    __builtin_nontemporal_store(cb[j][2], r + 2);
                 }
             }
         }
@@ -1326,16 +1343,36 @@ struct Fix4 {
     uint16_t rf;
 };
 
+template <int FMT>
 __device__ __forceinline__ void fix4_load(const BackArgs& a, int t, int row, int bx, bool act, Fix4& b)
 {
     const int bxc = act ? bx : 0, rowc = act ? row : 0;   // inactive lanes load a valid block, unused
-    const uint8_t* f = a.bgr + (size_t)t * a.fstride + (size_t)(rowc * 4) * a.pitch + 12 * (size_t)bxc;
+    if constexpr (FMT == DVC_FMT_BGR) {
+        const uint8_t* f = a.bgr + (size_t)t * a.fstride + (size_t)(rowc * 4) * a.pitch + 12 * (size_t)bxc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)i * a.pitch);
-        b.px[i][0] = v.x;
-        b.px[i][1] = v.y;
-        b.px[i][2] = v.z;
+        for (int i = 0; i < 4; ++i) {
+            const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)i * a.pitch);
+            b.px[i][0] = v.x;
+            b.px[i][1] = v.y;
+            b.px[i][2] = v.z;
+        }
+    } else {   // a 4:2:0 surface read in place: the quad's luma dword and its chroma, as k_front
+        const uint8_t* f = a.bgr + (size_t)t * a.fstride;
+        const int xq = 4 * bxc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int y = 4 * rowc + i;
+            const uint32_t y4 = *reinterpret_cast<const uint32_t*>(f + (size_t)y * a.pitch + xq);
+            const uint8_t* cr = f + a.sf.uoff + (size_t)(y >> 1) * a.sf.cpitch + (FMT == DVC_FMT_NV12 ? xq : xq / 2);
+            uint32_t c1, c2 = 0;
+            if constexpr (FMT == DVC_FMT_NV12) {
+                c1 = *reinterpret_cast<const uint32_t*>(cr);
+            } else {
+                c1 = *reinterpret_cast<const uint16_t*>(cr);
+                c2 = *reinterpret_cast<const uint16_t*>(cr + (a.sf.voff - a.sf.uoff));
+            }
+            quad_bgr<FMT>(y4, c1, c2, b.px[i]);
+        }
     }
     b.rf = a.overlay ? reinterpret_cast<const uint16_t*>(a.rblk)[(size_t)t * a.NBY * a.NBX + (size_t)rowc * a.NBX + bxc]
                      : (uint16_t)0;
@@ -1404,6 +1441,7 @@ __device__ __forceinline__ int select_bit(uint64_t m, int r)
     return base + __builtin_ctz(v);
 }
 
+template <int FMT>
 __global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
 {
     const int lane = threadIdx.x & 63;
@@ -1440,7 +1478,7 @@ __global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
             const int bit = act ? select_bit(m, j - excl) : 0;
             const int row = row0 + s / SW, bx = (s % SW) * 64 + bit;
             Fix4 b;
-            fix4_load(a, t, row, bx, act, b);
+            fix4_load<FMT>(a, t, row, bx, act, b);
             if (act) fix4_store(a, t, row, bx, b);
         }
     }
@@ -1774,7 +1812,13 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
             // DVC_FRONT_LDS=<bytes> (experiment): unused dynamic LDS per workgroup, to
             // cap the fused front's workgroups per CU and leave room to the others
             static const size_t pad = [] { const char* e = getenv("DVC_FRONT_LDS"); return e ? (size_t)atol(e) : 0; }();
-            if (pf == 2 && NW == 4)
+            if (sf.fmt == DVC_FMT_NV12)
+                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                                   chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+            else if (sf.fmt == DVC_FMT_I420)
+                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                                   chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+            else if (pf == 2 && NW == 4)
                 hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             else
@@ -1801,7 +1845,6 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const Src
                         uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s,
                         const FrontOut* fo)
 {
-    if (fo && sf.fmt != DVC_FMT_BGR) return hipErrorInvalidValue;   // fused outputs: BGR frames only
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
     if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
@@ -1967,8 +2010,8 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
     const int ntx = (a.g.W + 64 * B - 1) / (64 * B), nty = (a.g.H + 4 * B - 1) / (4 * B);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
     const int f = a.sf.fmt;
-    if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR in and out, dword rows)
-        if (B != 4 || f != DVC_FMT_BGR || a.out_i420 || a.obytes) return hipErrorInvalidValue;
+    if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR out in dword rows)
+        if (B != 4 || a.out_i420 || a.obytes) return hipErrorInvalidValue;
         static const int fwgs = [] {   // DVC_FIX_WGS: k_fix4 workgroups (default 6 per CU: all resident at 79 VGPRs)
             if (const char* e = getenv("DVC_FIX_WGS")) return std::max(1, atoi(e));
             int dev = 0, cus = 256;
@@ -1979,7 +2022,10 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
         }();
         if (a.SW > 64) return hipErrorInvalidValue;   // rows of <= 64 words (W <= 16384 px): the scan's lanes
         const int RG = std::max(1, 64 / a.SW), units = (a.NBY + RG - 1) / RG * a.n;
-        hipLaunchKernelGGL(k_fix4, dim3(std::max(1, std::min(fwgs, (units + 3) / 4))), dim3(256), 0, s, a, RG);
+        const dim3 fg(std::max(1, std::min(fwgs, (units + 3) / 4)));
+        if (a.sf.fmt == DVC_FMT_NV12) hipLaunchKernelGGL(k_fix4<DVC_FMT_NV12>, fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_I420) hipLaunchKernelGGL(k_fix4<DVC_FMT_I420>, fg, dim3(256), 0, s, a, RG);
+        else hipLaunchKernelGGL(k_fix4<DVC_FMT_BGR>, fg, dim3(256), 0, s, a, RG);
     }
     else if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);

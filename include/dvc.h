@@ -83,8 +83,9 @@ extern "C" {
                                      front's speculative static-block outputs +
                                      k_fix4 (same bytes; the fused form reads each
                                      frame from HBM once instead of twice. It
-                                     applies to block_size 4, BGR frames in and
-                                     out, 4-byte aligned output rows; the
+                                     applies to block_size 4, BGR frames or
+                                     4:2:0 surfaces read in place, BGR outputs
+                                     in 4-byte aligned rows; the
                                      environment variable DVC_FD_FUSED=0 sets
                                      this flag for every handle)                */
 

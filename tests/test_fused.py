@@ -1,14 +1,14 @@
 """GPU parity of the fused front (fd_kernels.h FrontOut) against the one-pass
 output stage, through the C-ABI.
 
-With block_size 4 and BGR frames in and out, k_front writes every full 4x4
+With block_size 4 and BGR outputs (BGR or 4:2:0 input), k_front writes every full 4x4
 block of both outputs as if it were static (overlay = the frame, compressed =
 (Y', Y', Y') of the quantised DCT, frame_differencing.py:110-130) while it has
-the frame in registers, and k_fix rewrites the blocks the accumulated mask
+the frame in registers, and k_fix4 rewrites the blocks the accumulated mask
 makes non-static. The bytes must equal the unfused k_out pass
 (DVC_FLAG_FD_UNFUSED) and the oracle, including when a caller reuses output
 buffers across calls — a later batch's speculative stores must not land
-before an earlier batch's k_fix of the same bytes.
+before an earlier batch's k_fix4 of the same bytes.
 """
 import numpy as np
 import pytest
@@ -113,3 +113,44 @@ def test_fused_reused_output_buffers(gpu_lib, oracle_lib):
         ov, cp = ring[c % 2]
         assert np.array_equal(ov[j].cpu().numpy(), rov), f"overlay != oracle: chunk {c} frame {j}"
         assert np.array_equal(cp[j].cpu().numpy(), rcp), f"compressed != oracle: chunk {c} frame {j}"
+
+
+@pytest.mark.parametrize("fmt", ["NV12", "I420"])
+def test_fused_yuv_surfaces(gpu_lib, oracle_lib, fmt):
+    """4:2:0 decoder surfaces read in place: the fused front converts each
+    block's quads once (gray and overlay) and k_fix4 converts the non-static
+    blocks it rewrites; every byte equals the one-pass path's."""
+    import ctypes
+    import torch
+    from dvc_amd.synthetic import clip
+    from tests.test_video_io_gpu import _nv12, _surface
+    N = gpu_lib._native
+    W, H, pitch, crows, n, batch = 1280, 720, 1408, 736, 41, 20
+    frames = clip(W, H, n, seed=12, noisy=True)
+    i420 = np.stack([oracle_lib.bgr_to_i420(f) for f in frames])
+    surf = np.stack([_surface(f if fmt == "I420" else _nv12(f, H, W), H, W, fmt, pitch, crows) for f in i420])
+    d = torch.from_numpy(surf).cuda()
+    L = N.lib()
+    outs = {}
+    for fused in (True, False):
+        p = gpu_lib.fd.derive_params(W, H, in_format=fmt, chroma_rows=crows,
+                                     flags=N.DVC_FLAG_DEVICE_PTRS | N.DVC_FLAG_KTIMING |
+                                     (0 if fused else N.DVC_FLAG_FD_UNFUSED))
+        p.max_batch = batch
+        ov = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device="cuda")
+        cp = torch.empty_like(ov)
+        h = ctypes.c_void_p()
+        N.check(L.dvc_fd_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+        try:
+            N.check(L.dvc_fd_prime(h, d[0].data_ptr(), pitch))
+            N.check(L.dvc_fd_step_batch(h, d[1].data_ptr(), pitch, surf[0].nbytes, n - 1, ov.data_ptr(),
+                                        cp.data_ptr(), 3 * W * H))
+            N.check(L.dvc_fd_sync(h))
+            kk = L.dvc_fd_ktime_kernel(h)
+        finally:
+            L.dvc_fd_destroy(h)
+        assert kk == (N.KTIME_FRONT_FUSED if fused else N.KTIME_OUT)
+        outs[fused] = (ov, cp)
+    for t in range(n - 1):
+        assert torch.equal(outs[True][0][t], outs[False][0][t]), f"overlay: fused != unfused at frame {t + 1}"
+        assert torch.equal(outs[True][1][t], outs[False][1][t]), f"compressed: fused != unfused at frame {t + 1}"

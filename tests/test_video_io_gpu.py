@@ -159,6 +159,7 @@ def test_fd_nv12_device_surfaces_and_resize(gpu_lib, oracle_lib):
 
 @pytest.mark.parametrize("fmt,W,H,pitch,crows,block,batch", [
     ("I420", 1920, 1080, 2048, 1088, 4, 3),   # decoder surface, fast blocks, 2 launches + a partial one
+    ("NV12", 1920, 1080, 2048, 1088, 4, 5),   # the fused front reading NV12 in place (BGR outputs)
     ("NV12", 642, 362, 704, 368, 4, 4),       # W % 4 = 2, H % 4 = 2: partial edge blocks via k_out_gen
     ("I420", 640, 360, 640, 360, 6, 3),       # generic block size: k_out_gen only
     ("NV12", 646, 360, 648, 360, 8, 8),       # B = 8, right edge blocks 6 px wide
