@@ -154,3 +154,40 @@ def test_fused_yuv_surfaces(gpu_lib, oracle_lib, fmt):
     for t in range(n - 1):
         assert torch.equal(outs[True][0][t], outs[False][0][t]), f"overlay: fused != unfused at frame {t + 1}"
         assert torch.equal(outs[True][1][t], outs[False][1][t]), f"compressed: fused != unfused at frame {t + 1}"
+
+
+def test_fused_nv12_per_frame_partial_rows(gpu_lib, oracle_lib):
+    """NV12 surfaces stepped one frame a call (dvc_fd_step: one-frame batches of
+    the fused front) with H % 4 = 2 (the last block row partial: k_out_gen beside
+    k_fix4) and the same two output frames reused every call — each call's
+    speculative stores wait for the previous call's fix-up — against the oracle
+    on the converted frames."""
+    import ctypes
+    import torch
+    from dvc_amd.synthetic import clip
+    from tests.test_video_io_gpu import _nv12, _oracle_run, _surface
+    N = gpu_lib._native
+    W, H, pitch, crows, n = 640, 362, 704, 368, 9
+    frames = clip(W, H, n, seed=14, noisy=True)
+    i420 = np.stack([oracle_lib.bgr_to_i420(f) for f in frames])
+    bgr = np.stack([oracle_lib.yuv420_to_bgr(f) for f in i420])
+    outs, _ = _oracle_run(oracle_lib, bgr, W, H)
+    surf = np.stack([_surface(_nv12(f, H, W), H, W, "NV12", pitch, crows) for f in i420])
+    d = torch.from_numpy(surf).cuda()
+    p = gpu_lib.fd.derive_params(W, H, in_format="NV12", chroma_rows=crows,
+                                 flags=N.DVC_FLAG_DEVICE_PTRS | N.DVC_FLAG_KTIMING)
+    L = N.lib()
+    h = ctypes.c_void_p()
+    N.check(L.dvc_fd_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+    ov = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+    cp = torch.empty_like(ov)
+    try:
+        N.check(L.dvc_fd_prime(h, d[0].data_ptr(), pitch))
+        for t in range(1, n):
+            N.check(L.dvc_fd_step(h, d[t].data_ptr(), pitch, ov.data_ptr(), cp.data_ptr(), None))
+            N.check(L.dvc_fd_sync(h))
+            assert L.dvc_fd_ktime_kernel(h) == N.KTIME_FRONT_FUSED
+            assert np.array_equal(ov.cpu().numpy(), outs[t - 1][0]), f"overlay differs at frame {t}"
+            assert np.array_equal(cp.cpu().numpy(), outs[t - 1][1]), f"compressed differs at frame {t}"
+    finally:
+        L.dvc_fd_destroy(h)
