@@ -191,3 +191,49 @@ def test_fused_nv12_per_frame_partial_rows(gpu_lib, oracle_lib):
             assert np.array_equal(cp.cpu().numpy(), outs[t - 1][1]), f"compressed differs at frame {t}"
     finally:
         L.dvc_fd_destroy(h)
+
+
+def test_fused_nv12_bench_scale(gpu_lib, oracle_lib):
+    """The NV12 bench configuration (1080p, 383-frame launches, two launches a
+    call, two calls into the same outputs): the fused front's outputs and stats
+    equal the one-pass path's (itself pinned against the oracle by
+    test_video_io_gpu.py) over 1532 frames."""
+    import ctypes
+    import torch
+    from dvc_amd.synthetic import clip
+    from tests.test_video_io_gpu import _nv12
+    N = gpu_lib._native
+    W, H, R, batch = 1920, 1080, 48, 383
+    frames = clip(W, H, R, seed=3)
+    nv = np.stack([_nv12(oracle_lib.bgr_to_i420(f), H, W) for f in frames])   # (R, 1.5H, W)
+    order = list(range(R)) + list(range(R - 2, 0, -1))
+    P = 766
+    idx = torch.tensor([order[(j + 1) % len(order)] for j in range(P)], device="cuda")
+    ring = torch.from_numpy(nv).cuda()
+    seq = ring[idx].contiguous()
+    L = N.lib()
+    outs = {}
+    for fused in (True, False):
+        p = gpu_lib.fd.derive_params(W, H, in_format="NV12", chroma_rows=H,
+                                     flags=N.DVC_FLAG_DEVICE_PTRS | (0 if fused else N.DVC_FLAG_FD_UNFUSED))
+        p.max_batch = batch
+        ov = torch.empty((P, H, W, 3), dtype=torch.uint8, device="cuda")
+        cp = torch.empty_like(ov)
+        h = ctypes.c_void_p()
+        N.check(L.dvc_fd_create(ctypes.byref(p), 0, None, ctypes.byref(h)))
+        try:
+            N.check(L.dvc_fd_prime(h, ring[0].data_ptr(), W))
+            for _ in range(2):
+                N.check(L.dvc_fd_step_batch(h, seq.data_ptr(), W, nv[0].nbytes, P, ov.data_ptr(), cp.data_ptr(),
+                                            3 * W * H))
+            N.check(L.dvc_fd_sync(h))
+            st = N.FdStats()
+            N.check(L.dvc_fd_get_stats(h, ctypes.byref(st)))
+        finally:
+            L.dvc_fd_destroy(h)
+        outs[fused] = (ov, cp, {k: int(getattr(st, k)) for k, _ in st._fields_})
+    assert outs[True][2] == outs[False][2]
+    for t in range(P):
+        assert torch.equal(outs[True][0][t], outs[False][0][t]), f"overlay: fused != unfused at frame {t}"
+        assert torch.equal(outs[True][1][t], outs[False][1][t]), f"compressed: fused != unfused at frame {t}"
+    del outs, seq, ring
