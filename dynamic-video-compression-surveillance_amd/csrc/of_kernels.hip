@@ -1662,6 +1662,49 @@ __global__ void __launch_bounds__(256) k_of_rect(OfGeom g, OfBufs B)
     }
 }
 
+// The 8x8 DCT basis as dct_matrix(8) builds it on the host (fd_api.hip:
+// (float)(c * cos(pi (2n+1) k / 16))), as compile-time constants: k_of_out's
+// DCT passes take their factors as literals instead of 128 kernel-argument
+// SGPRs (which spilled). of_launch_out checks OfOutArgs::M bit for bit.
+__device__ constexpr DctMat kDct8 = {
+    {0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
+    0x1.f6297cp-2f, 0x1.a9b662p-2f, 0x1.1c73b4p-2f, 0x1.8f8b84p-4f, -0x1.8f8b84p-4f, -0x1.1c73b4p-2f, -0x1.a9b662p-2f, -0x1.f6297cp-2f,
+    0x1.d906bcp-2f, 0x1.87de2ap-3f, -0x1.87de2ap-3f, -0x1.d906bcp-2f, -0x1.d906bcp-2f, -0x1.87de2ap-3f, 0x1.87de2ap-3f, 0x1.d906bcp-2f,
+    0x1.a9b662p-2f, -0x1.8f8b84p-4f, -0x1.f6297cp-2f, -0x1.1c73b4p-2f, 0x1.1c73b4p-2f, 0x1.f6297cp-2f, 0x1.8f8b84p-4f, -0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
+    0x1.1c73b4p-2f, -0x1.f6297cp-2f, 0x1.8f8b84p-4f, 0x1.a9b662p-2f, -0x1.a9b662p-2f, -0x1.8f8b84p-4f, 0x1.f6297cp-2f, -0x1.1c73b4p-2f,
+    0x1.87de2ap-3f, -0x1.d906bcp-2f, 0x1.d906bcp-2f, -0x1.87de2ap-3f, -0x1.87de2ap-3f, 0x1.d906bcp-2f, -0x1.d906bcp-2f, 0x1.87de2ap-3f,
+    0x1.8f8b84p-4f, -0x1.1c73b4p-2f, 0x1.a9b662p-2f, -0x1.f6297cp-2f, 0x1.f6297cp-2f, -0x1.a9b662p-2f, 0x1.1c73b4p-2f, -0x1.8f8b84p-4f},
+    {0x1.6a09e6p-2f, 0x1.f6297cp-2f, 0x1.d906bcp-2f, 0x1.a9b662p-2f, 0x1.6a09e6p-2f, 0x1.1c73b4p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f,
+    0x1.6a09e6p-2f, 0x1.a9b662p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f, -0x1.6a09e6p-2f, -0x1.f6297cp-2f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f,
+    0x1.6a09e6p-2f, 0x1.1c73b4p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f, -0x1.6a09e6p-2f, 0x1.8f8b84p-4f, 0x1.d906bcp-2f, 0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, 0x1.8f8b84p-4f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f, 0x1.6a09e6p-2f, 0x1.a9b662p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f,
+    0x1.6a09e6p-2f, -0x1.8f8b84p-4f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f, 0x1.6a09e6p-2f, -0x1.a9b662p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f,
+    0x1.6a09e6p-2f, -0x1.1c73b4p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f, -0x1.6a09e6p-2f, -0x1.8f8b84p-4f, 0x1.d906bcp-2f, -0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, -0x1.a9b662p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f, -0x1.6a09e6p-2f, 0x1.f6297cp-2f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f,
+    0x1.6a09e6p-2f, -0x1.f6297cp-2f, 0x1.d906bcp-2f, -0x1.a9b662p-2f, 0x1.6a09e6p-2f, -0x1.1c73b4p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f}};
+static constexpr float kDct8Host[128] = {
+    0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
+    0x1.f6297cp-2f, 0x1.a9b662p-2f, 0x1.1c73b4p-2f, 0x1.8f8b84p-4f, -0x1.8f8b84p-4f, -0x1.1c73b4p-2f, -0x1.a9b662p-2f, -0x1.f6297cp-2f,
+    0x1.d906bcp-2f, 0x1.87de2ap-3f, -0x1.87de2ap-3f, -0x1.d906bcp-2f, -0x1.d906bcp-2f, -0x1.87de2ap-3f, 0x1.87de2ap-3f, 0x1.d906bcp-2f,
+    0x1.a9b662p-2f, -0x1.8f8b84p-4f, -0x1.f6297cp-2f, -0x1.1c73b4p-2f, 0x1.1c73b4p-2f, 0x1.f6297cp-2f, 0x1.8f8b84p-4f, -0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
+    0x1.1c73b4p-2f, -0x1.f6297cp-2f, 0x1.8f8b84p-4f, 0x1.a9b662p-2f, -0x1.a9b662p-2f, -0x1.8f8b84p-4f, 0x1.f6297cp-2f, -0x1.1c73b4p-2f,
+    0x1.87de2ap-3f, -0x1.d906bcp-2f, 0x1.d906bcp-2f, -0x1.87de2ap-3f, -0x1.87de2ap-3f, 0x1.d906bcp-2f, -0x1.d906bcp-2f, 0x1.87de2ap-3f,
+    0x1.8f8b84p-4f, -0x1.1c73b4p-2f, 0x1.a9b662p-2f, -0x1.f6297cp-2f, 0x1.f6297cp-2f, -0x1.a9b662p-2f, 0x1.1c73b4p-2f, -0x1.8f8b84p-4f,
+    0x1.6a09e6p-2f, 0x1.f6297cp-2f, 0x1.d906bcp-2f, 0x1.a9b662p-2f, 0x1.6a09e6p-2f, 0x1.1c73b4p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f,
+    0x1.6a09e6p-2f, 0x1.a9b662p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f, -0x1.6a09e6p-2f, -0x1.f6297cp-2f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f,
+    0x1.6a09e6p-2f, 0x1.1c73b4p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f, -0x1.6a09e6p-2f, 0x1.8f8b84p-4f, 0x1.d906bcp-2f, 0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, 0x1.8f8b84p-4f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f, 0x1.6a09e6p-2f, 0x1.a9b662p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f,
+    0x1.6a09e6p-2f, -0x1.8f8b84p-4f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f, 0x1.6a09e6p-2f, -0x1.a9b662p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f,
+    0x1.6a09e6p-2f, -0x1.1c73b4p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f, -0x1.6a09e6p-2f, -0x1.8f8b84p-4f, 0x1.d906bcp-2f, -0x1.a9b662p-2f,
+    0x1.6a09e6p-2f, -0x1.a9b662p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f, -0x1.6a09e6p-2f, 0x1.f6297cp-2f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f,
+    0x1.6a09e6p-2f, -0x1.f6297cp-2f, 0x1.d906bcp-2f, -0x1.a9b662p-2f, 0x1.6a09e6p-2f, -0x1.1c73b4p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f};
+static bool dct8_is_const(const DctMat& M)
+{
+    return std::memcmp(M.m, kDct8Host, 64 * sizeof(float)) == 0 && std::memcmp(M.mt, kDct8Host + 64, 64 * sizeof(float)) == 0;
+}
+
 // k_of_out: one group of 8 lanes per 8x8 block (lane r = row r of the block),
 // 8 blocks side by side per wave (64 px x 8 rows), 4 waves = 4 block rows.
 // Per static full block and channel (of:156-168) the separable DCT, quantiser
@@ -1792,23 +1835,23 @@ __global__ void __launch_bounds__(256) k_of_out(OfGeom g, OfBufs B, OfOutArgs o)
             float x[8], v[8], u[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = (float)cc[j] - 128.0f;
-            dct_rows8(x, o.M, v);            // T row r
+            dct_rows8(x, kDct8, v);            // T row r
             transpose8(S, r, v, u);          // T column r: u[i] = T[i][r]
 #pragma unroll
             for (int k = 0; k < 8; ++k) {    // X[k][r] = rint(sum_i M[k][i] T[i][r] / q) q
-                float tt = o.M.m[k * 8] * u[0];
+                float tt = kDct8.m[k * 8] * u[0];
 #pragma unroll
-                for (int i = 1; i < 8; ++i) tt = __builtin_fmaf(o.M.m[k * 8 + i], u[i], tt);
+                for (int i = 1; i < 8; ++i) tt = __builtin_fmaf(kDct8.m[k * 8 + i], u[i], tt);
                 v[k] = __builtin_rintf(div_rn(tt, o.qinv)) * o.quant;
             }
             transpose8(S, r, v, x);          // X row r
-            idct_rows8(x, o.M, v);           // T2 row r
+            idct_rows8(x, kDct8, v);           // T2 row r
             transpose8(S, r, v, u);          // T2 column r
 #pragma unroll
             for (int i = 0; i < 8; ++i) {    // X[i][r] = sum_k M[k][i] T2[k][r]
-                float tt = o.M.m[i] * u[0];
+                float tt = kDct8.m[i] * u[0];
 #pragma unroll
-                for (int k = 1; k < 8; ++k) tt = __builtin_fmaf(o.M.m[k * 8 + i], u[k], tt);
+                for (int k = 1; k < 8; ++k) tt = __builtin_fmaf(kDct8.m[k * 8 + i], u[k], tt);
                 v[i] = tt;
             }
             transpose8(S, r, v, x);          // row r of the reconstruction
@@ -2221,6 +2264,7 @@ hipError_t of_launch_mask(const OfGeom& g, const OfBufs& b, long long a0, int wi
 hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, int n, hipStream_t s)
 {
     if (!o.mask && !o.compressed) return hipSuccess;
+    if (!dct8_is_const(o.M)) return hipErrorInvalidValue;   // k_of_out's constant basis
     const int nbx = (g.W + 7) / 8, nby = (g.H + 7) / 8;   // partial edge blocks included (pixels, not DCT)
     dim3 grid((nbx + 7) / 8, (nby + 3) / 4, n);
     hipLaunchKernelGGL(k_of_out, grid, dim3(256), 0, s, g, b, o);
