@@ -34,6 +34,7 @@
 
 #include "dvc_device.h"
 #include "fd_kernels.h"
+#include "dct_const.h"
 #include "yuv_px.h"
 #include "../../include/dvc.h"
 
@@ -131,28 +132,6 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 // surfaces: converted to BGR once, for the overlay and the gray), its gray
 // quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
 // the compressed frame.
-// The 4x4 DCT basis as dct_matrix(4) builds it on the host (fd_api.hip:
-// (float)(c * cos(pi (2n+1) k / 8))), as compile-time constants: the fused
-// front's DCT then takes its factors as literals / inline constants instead
-// of 32 kernel-argument SGPRs. launch_front checks FrontOut::M against it
-// bit for bit and refuses the fused form otherwise (dct4_is_const).
-#define DVC_A4 0x1.4e7aeap-1f
-#define DVC_B4 0x1.1517a8p-2f
-__device__ constexpr DctMat kDct4 = {
-    {0.5f, 0.5f, 0.5f, 0.5f, DVC_A4, DVC_B4, -DVC_B4, -DVC_A4, 0.5f, -0.5f, -0.5f, 0.5f, DVC_B4, -DVC_A4, DVC_A4, -DVC_B4},
-    {0.5f, DVC_A4, 0.5f, DVC_B4, 0.5f, DVC_B4, -0.5f, -DVC_A4, 0.5f, -DVC_B4, -0.5f, DVC_A4, 0.5f, -DVC_A4, 0.5f, -DVC_B4}};
-static constexpr float kDct4Host[32] = {
-    0.5f, 0.5f, 0.5f, 0.5f, DVC_A4, DVC_B4, -DVC_B4, -DVC_A4, 0.5f, -0.5f, -0.5f, 0.5f, DVC_B4, -DVC_A4, DVC_A4, -DVC_B4,
-    0.5f, DVC_A4, 0.5f, DVC_B4, 0.5f, DVC_B4, -0.5f, -DVC_A4, 0.5f, -DVC_B4, -0.5f, DVC_A4, 0.5f, -DVC_A4, 0.5f, -DVC_B4};
-#undef DVC_A4
-#undef DVC_B4
-
-static bool dct4_is_const(const DctMat& M)
-{
-    return std::memcmp(M.m, kDct4Host, 16 * sizeof(float)) == 0 &&
-           std::memcmp(M.mt, kDct4Host + 16, 16 * sizeof(float)) == 0;
-}
-
 template <int NW, int PF, int FMT, bool OUT>
 __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
@@ -1298,7 +1277,7 @@ __device__ __forceinline__ void out_tile(const BackArgs& a, int t, int tx, int t
                     for (int j = 0; j < 4; ++j) X[i * B + 4 * qd + j] = (float)((int)y[j] - 128);
                 }
             if constexpr (B == 4) block_dct_quant_pk<B>(X, kDct4, a.quant, a.qinv);   // (launch_out checks a.M)
-            else block_dct_quant<B>(X, a.M, a.quant, a.qinv);   // B = 8: the packed form spills
+            else block_dct_quant<B>(X, kDct8, a.quant, a.qinv);   // B = 8 (the packed form spills); launch_out checks a.M
 #pragma unroll
             for (int i = 0; i < B; ++i)
 #pragma unroll
@@ -2011,7 +1990,8 @@ static void launch_gen(const BackArgs& a, int rx0, int rx1, int ry0, int ry1, in
 hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
 {
     const int B = a.B;
-    if (B == 4 && !dct4_is_const(a.M)) return hipErrorInvalidValue;   // k_out<4>'s constant basis
+    if ((B == 4 && !dct4_is_const(a.M)) || (B == 8 && !dct8_is_const(a.M)))
+        return hipErrorInvalidValue;   // k_out<4> / k_out<8>'s constant bases
     const int per = std::max(1, 1024 / (B * B));             // blocks of a ~1024-px job
     if (!fast_block(B)) {
         int jb = 1;

@@ -37,6 +37,7 @@
 #include "../../include/dvc.h"
 #include "dvc_device.h"
 #include "of_kernels.h"
+#include "dct_const.h"
 #include "yuv_px.h"
 
 namespace dvc {
@@ -1660,49 +1661,6 @@ __global__ void __launch_bounds__(256) k_of_rect(OfGeom g, OfBufs B)
             atomicOr(reinterpret_cast<unsigned long long*>(rb + (size_t)row * g.WW + wi), (unsigned long long)mk);
         }
     }
-}
-
-// The 8x8 DCT basis as dct_matrix(8) builds it on the host (fd_api.hip:
-// (float)(c * cos(pi (2n+1) k / 16))), as compile-time constants: k_of_out's
-// DCT passes take their factors as literals instead of 128 kernel-argument
-// SGPRs (which spilled). of_launch_out checks OfOutArgs::M bit for bit.
-__device__ constexpr DctMat kDct8 = {
-    {0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
-    0x1.f6297cp-2f, 0x1.a9b662p-2f, 0x1.1c73b4p-2f, 0x1.8f8b84p-4f, -0x1.8f8b84p-4f, -0x1.1c73b4p-2f, -0x1.a9b662p-2f, -0x1.f6297cp-2f,
-    0x1.d906bcp-2f, 0x1.87de2ap-3f, -0x1.87de2ap-3f, -0x1.d906bcp-2f, -0x1.d906bcp-2f, -0x1.87de2ap-3f, 0x1.87de2ap-3f, 0x1.d906bcp-2f,
-    0x1.a9b662p-2f, -0x1.8f8b84p-4f, -0x1.f6297cp-2f, -0x1.1c73b4p-2f, 0x1.1c73b4p-2f, 0x1.f6297cp-2f, 0x1.8f8b84p-4f, -0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
-    0x1.1c73b4p-2f, -0x1.f6297cp-2f, 0x1.8f8b84p-4f, 0x1.a9b662p-2f, -0x1.a9b662p-2f, -0x1.8f8b84p-4f, 0x1.f6297cp-2f, -0x1.1c73b4p-2f,
-    0x1.87de2ap-3f, -0x1.d906bcp-2f, 0x1.d906bcp-2f, -0x1.87de2ap-3f, -0x1.87de2ap-3f, 0x1.d906bcp-2f, -0x1.d906bcp-2f, 0x1.87de2ap-3f,
-    0x1.8f8b84p-4f, -0x1.1c73b4p-2f, 0x1.a9b662p-2f, -0x1.f6297cp-2f, 0x1.f6297cp-2f, -0x1.a9b662p-2f, 0x1.1c73b4p-2f, -0x1.8f8b84p-4f},
-    {0x1.6a09e6p-2f, 0x1.f6297cp-2f, 0x1.d906bcp-2f, 0x1.a9b662p-2f, 0x1.6a09e6p-2f, 0x1.1c73b4p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f,
-    0x1.6a09e6p-2f, 0x1.a9b662p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f, -0x1.6a09e6p-2f, -0x1.f6297cp-2f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f,
-    0x1.6a09e6p-2f, 0x1.1c73b4p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f, -0x1.6a09e6p-2f, 0x1.8f8b84p-4f, 0x1.d906bcp-2f, 0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, 0x1.8f8b84p-4f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f, 0x1.6a09e6p-2f, 0x1.a9b662p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f,
-    0x1.6a09e6p-2f, -0x1.8f8b84p-4f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f, 0x1.6a09e6p-2f, -0x1.a9b662p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f,
-    0x1.6a09e6p-2f, -0x1.1c73b4p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f, -0x1.6a09e6p-2f, -0x1.8f8b84p-4f, 0x1.d906bcp-2f, -0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, -0x1.a9b662p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f, -0x1.6a09e6p-2f, 0x1.f6297cp-2f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f,
-    0x1.6a09e6p-2f, -0x1.f6297cp-2f, 0x1.d906bcp-2f, -0x1.a9b662p-2f, 0x1.6a09e6p-2f, -0x1.1c73b4p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f}};
-static constexpr float kDct8Host[128] = {
-    0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
-    0x1.f6297cp-2f, 0x1.a9b662p-2f, 0x1.1c73b4p-2f, 0x1.8f8b84p-4f, -0x1.8f8b84p-4f, -0x1.1c73b4p-2f, -0x1.a9b662p-2f, -0x1.f6297cp-2f,
-    0x1.d906bcp-2f, 0x1.87de2ap-3f, -0x1.87de2ap-3f, -0x1.d906bcp-2f, -0x1.d906bcp-2f, -0x1.87de2ap-3f, 0x1.87de2ap-3f, 0x1.d906bcp-2f,
-    0x1.a9b662p-2f, -0x1.8f8b84p-4f, -0x1.f6297cp-2f, -0x1.1c73b4p-2f, 0x1.1c73b4p-2f, 0x1.f6297cp-2f, 0x1.8f8b84p-4f, -0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f, 0x1.6a09e6p-2f, -0x1.6a09e6p-2f, -0x1.6a09e6p-2f, 0x1.6a09e6p-2f,
-    0x1.1c73b4p-2f, -0x1.f6297cp-2f, 0x1.8f8b84p-4f, 0x1.a9b662p-2f, -0x1.a9b662p-2f, -0x1.8f8b84p-4f, 0x1.f6297cp-2f, -0x1.1c73b4p-2f,
-    0x1.87de2ap-3f, -0x1.d906bcp-2f, 0x1.d906bcp-2f, -0x1.87de2ap-3f, -0x1.87de2ap-3f, 0x1.d906bcp-2f, -0x1.d906bcp-2f, 0x1.87de2ap-3f,
-    0x1.8f8b84p-4f, -0x1.1c73b4p-2f, 0x1.a9b662p-2f, -0x1.f6297cp-2f, 0x1.f6297cp-2f, -0x1.a9b662p-2f, 0x1.1c73b4p-2f, -0x1.8f8b84p-4f,
-    0x1.6a09e6p-2f, 0x1.f6297cp-2f, 0x1.d906bcp-2f, 0x1.a9b662p-2f, 0x1.6a09e6p-2f, 0x1.1c73b4p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f,
-    0x1.6a09e6p-2f, 0x1.a9b662p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f, -0x1.6a09e6p-2f, -0x1.f6297cp-2f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f,
-    0x1.6a09e6p-2f, 0x1.1c73b4p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f, -0x1.6a09e6p-2f, 0x1.8f8b84p-4f, 0x1.d906bcp-2f, 0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, 0x1.8f8b84p-4f, -0x1.d906bcp-2f, -0x1.1c73b4p-2f, 0x1.6a09e6p-2f, 0x1.a9b662p-2f, -0x1.87de2ap-3f, -0x1.f6297cp-2f,
-    0x1.6a09e6p-2f, -0x1.8f8b84p-4f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f, 0x1.6a09e6p-2f, -0x1.a9b662p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f,
-    0x1.6a09e6p-2f, -0x1.1c73b4p-2f, -0x1.87de2ap-3f, 0x1.f6297cp-2f, -0x1.6a09e6p-2f, -0x1.8f8b84p-4f, 0x1.d906bcp-2f, -0x1.a9b662p-2f,
-    0x1.6a09e6p-2f, -0x1.a9b662p-2f, 0x1.87de2ap-3f, 0x1.8f8b84p-4f, -0x1.6a09e6p-2f, 0x1.f6297cp-2f, -0x1.d906bcp-2f, 0x1.1c73b4p-2f,
-    0x1.6a09e6p-2f, -0x1.f6297cp-2f, 0x1.d906bcp-2f, -0x1.a9b662p-2f, 0x1.6a09e6p-2f, -0x1.1c73b4p-2f, 0x1.87de2ap-3f, -0x1.8f8b84p-4f};
-static bool dct8_is_const(const DctMat& M)
-{
-    return std::memcmp(M.m, kDct8Host, 64 * sizeof(float)) == 0 && std::memcmp(M.mt, kDct8Host + 64, 64 * sizeof(float)) == 0;
 }
 
 // k_of_out: one group of 8 lanes per 8x8 block (lane r = row r of the block),
