@@ -277,6 +277,17 @@ __device__ __forceinline__ void row_pair_unions(int W, int WW, const RowIdx& r0,
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// A per-lane 32-bit byte offset re-read where it is used: keeps (wave-uniform
+// base + zext(offset)) inside a loop body, so the access selects the SGPR-base
+// + VGPR-offset form (global_load/store ... v_off, s[base]) instead of one
+// 64-bit VALU add per access (LICM otherwise hoists the zext out of the loop
+// and the addition becomes a 64-bit VGPR pair per access).
+__device__ __forceinline__ uint32_t voff(uint32_t o)
+{
+    asm volatile("" : "+v"(o));
+    return o;
+}
+
 // RN_f32(t / q) from one double product: d = RN53(t * RN53(1/q)) is within
 // 2^-52 (relative) of t/q, while a float quotient t/q is never a float rounding
 // midpoint (that would need 25 significant bits) and, when not equal to one,

@@ -233,9 +233,17 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
             c = *reinterpret_cast<const uint16_t*>(f + co + dv);
         }
     };
+    // the offsets pass through voff in place once per frame (no copies): every
+    // load and store below is a uniform base + a 32-bit VGPR offset
     auto load = [&](Quads& qs, const uint8_t* f) {
 #pragma unroll
-        for (int j = 0; j < NR; ++j) load_quad(f, off[j], coff[j], qs.v0[j], qs.v1[j], qs.v2[j]);
+        for (int j = 0; j < NR; ++j) {
+            off[j] = voff(off[j]);
+            if constexpr (YUV) coff[j] = voff(coff[j]);
+            load_quad(f, off[j], coff[j], qs.v0[j], qs.v1[j], qs.v2[j]);
+        }
+        hoff = voff(hoff);
+        if constexpr (YUV) hcoff = voff(hcoff);
         load_quad(f, hoff, hcoff, qs.h0, qs.h1, qs.h2);
     };
     Quads qa, qb;
@@ -254,8 +262,20 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
     // OUT: this lane's block lies inside the frame (partial edge blocks are
     // k_out_gen's) and the frame is one of the chunk's (not its warm-up)
     const bool full_blk = OUT && x + 4 <= W && y0 + 4 * wave + 4 <= H;
-    const size_t orow0 = (size_t)(y0 + 4 * wave) * fo.opitch + 3 * (size_t)x;
+    // OUT rows and motion-bit words: per-lane 32-bit offsets from the frame's
+    // wave-uniform base (through voff once per frame, like the loads)
+    uint32_t oro[4], mwo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        oro[i] = OUT ? (uint32_t)((size_t)(y0 + 4 * wave + i) * fo.opitch + 3 * (size_t)x) : 0u;
+        mwo[i] = (uint32_t)(min(y0 + orow(i), H - 1) * WW + min((x0 >> 6) + (lane >> 4), WW - 1)) * 8u + ((lane >> 1) & 4u);
+    }
     auto frame = [&](Quads& qs, int t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if constexpr (OUT) oro[i] = voff(oro[i]);
+            mwo[i] = voff(mwo[i]);
+        }
         // OUT: the block's 4 rows as BGR (4:2:0 surfaces converted once, for
         // both the gray and the overlay); other rows straight to gray
         uint32_t cb[4][3];
@@ -280,10 +300,10 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
             // overlay := the frame (a static block has no acc > 127 pixel); the
             // registers are reloaded with frame t + PF right after the barrier
             if (fo.ov && full_blk && t >= t_first) {
-                uint8_t* o = fo.ov + (size_t)t * fo.ostride + orow0;
+                uint8_t* o = fo.ov + (size_t)t * fo.ostride;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    uint32_t* r = reinterpret_cast<uint32_t*>(o + (size_t)j * fo.opitch);
+                    uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[j]);
                     __builtin_nontemporal_store(cb[j][0], r);
                     __builtin_nontemporal_store(cb[j][1], r + 1);
                     __builtin_nontemporal_store(cb[j][2], r + 2);
@@ -369,7 +389,7 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
             w |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);
             const int wi = (x0 >> 6) + (lane >> 4);
             if ((lane & 7) == 0 && y < H && wi < WW && t >= t_first)
-                reinterpret_cast<uint32_t*>(mb)[((size_t)y * WW + wi) * 2 + ((lane >> 3) & 1)] = w;
+                *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(mb) + mwo[i]) = w;
         }
         // OUT: compressed := the block as static (fd:117-130): Y' = trunc(clip(
         // IDCT(rint(DCT(Y - 128) / q) q) + 128)), Cr = Cb = 128 -> (Y', Y', Y')
@@ -381,7 +401,7 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
 #pragma unroll
                     for (int j = 0; j < 4; ++j) X[4 * i + j] = (float)((int)((gq[i] >> (8 * j)) & 255u) - 128);
                 block_dct_quant_pk<4>(X, kDct4, fo.quant, fo.qinv);
-                uint8_t* o = fo.cp + (size_t)t * fo.ostride + orow0;
+                uint8_t* o = fo.cp + (size_t)t * fo.ostride;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     uint32_t u[4], cw[3];
@@ -389,7 +409,7 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(
                     for (int j = 0; j < 4; ++j)   // clip to [0, 255], truncating uint8 cast
                         u[j] = (uint32_t)__builtin_amdgcn_fmed3f(X[4 * i + j] + 128.0f, 0.0f, 255.0f);
                     gray_bgr4(u[0], u[1], u[2], u[3], cw);
-                    uint32_t* r = reinterpret_cast<uint32_t*>(o + (size_t)i * fo.opitch);
+                    uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[i]);
                     __builtin_nontemporal_store(cw[0], r);
                     __builtin_nontemporal_store(cw[1], r + 1);
                     __builtin_nontemporal_store(cw[2], r + 2);
