@@ -132,8 +132,17 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 // surfaces: converted to BGR once, for the overlay and the gray), its gray
 // quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
 // the compressed frame.
+// fused front workgroups per CU (the VGPR budget: 4 -> 128, 5 -> 96): BGR 4
+// (5 measured neutral, with scratch spills), 4:2:0 surfaces 5 (two loads a row:
+// the extra wave per SIMD hides them, +2.4 % NV12, experiments/README.md)
+#ifndef DVC_FRONT_WGS_BGR
+#define DVC_FRONT_WGS_BGR 4
+#endif
+#ifndef DVC_FRONT_WGS_YUV
+#define DVC_FRONT_WGS_YUV 5
+#endif
 template <int NW, int PF, int FMT, bool OUT>
-__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? 4 : 3) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : 3) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
@@ -1814,7 +1823,7 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     int chunks = (target / NW + tx * ty / 2) / (tx * ty);
     static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
     if (fo) {
-        // fused outputs (128 VGPRs: 4 workgroups per CU): chunks of ~48 frames
+        // fused outputs (4 workgroups per CU, 5 for 4:2:0 surfaces): chunks of ~48 frames
         // (1080p x 383: 8 chunks, 4352 workgroups; measured alone 373 k / 514 k /
         // 534 k Mpx/s at 1 / 4 / 8 chunks — a warm-up frame per chunk is 2 % more
         // reads, more workgroups in flight hide the per-frame barriers);
