@@ -376,10 +376,17 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR 
             const uint2 a0 = sh[rr][lane], a1 = sh[rr + 1][lane], a2 = sh[rr + 2][lane], a3 = sh[rr + 3][lane],
                         a4 = sh[rr + 4][lane];
             // 16-bit lanes: sum <= 16 * 4080 = 65280, packed adds cannot carry across halves
-            const u16x2 sx = as_u16x2(a0.x) + as_u16x2(a4.x) + ((as_u16x2(a1.x) + as_u16x2(a3.x)) << 2) +
-                             as_u16x2(a2.x) * (u16x2)6;
-            const u16x2 sy = as_u16x2(a0.y) + as_u16x2(a4.y) + ((as_u16x2(a1.y) + as_u16x2(a3.y)) << 2) +
-                             as_u16x2(a2.y) * (u16x2)6;
+            // 4 * (a1 + a3) + (6 * a2 + (a0 + a4)) as two v_pk_mad_u16 (the
+            // compiler turns * 4 back into a shift and an add)
+            auto vsum = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t b4) {
+                const uint32_t m = as_u32(as_u16x2(b2) * (u16x2)6 + (as_u16x2(b0) + as_u16x2(b4)));
+                const uint32_t p = as_u32(as_u16x2(b1) + as_u16x2(b3));
+                uint32_t r;
+                asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(p), "s"(0x00040004u), "v"(m));
+                return as_u16x2(r);
+            };
+            const u16x2 sx = vsum(a0.x, a1.x, a2.x, a3.x, a4.x);
+            const u16x2 sy = vsum(a0.y, a1.y, a2.y, a3.y, a4.y);
             const u16x2 gl = (sx + (u16x2)128) >> 8, gh = (sy + (u16x2)128) >> 8;
             const u16x2 dl = __builtin_elementwise_max(gl, pl[i]) - __builtin_elementwise_min(gl, pl[i]);
             const u16x2 dh = __builtin_elementwise_max(gh, ph[i]) - __builtin_elementwise_min(gh, ph[i]);
@@ -1378,11 +1385,13 @@ template <int FMT>
 __device__ __forceinline__ void fix4_load(const BackArgs& a, int t, int row, int bx, bool act, Fix4& b)
 {
     const int bxc = act ? bx : 0, rowc = act ? row : 0;   // inactive lanes load a valid block, unused
+    // wave-uniform frame bases + 32-bit per-lane offsets (SGPR-base addressing)
     if constexpr (FMT == DVC_FMT_BGR) {
-        const uint8_t* f = a.bgr + (size_t)t * a.fstride + (size_t)(rowc * 4) * a.pitch + 12 * (size_t)bxc;
+        const uint8_t* f = a.bgr + (size_t)t * a.fstride;
+        const uint32_t o = (uint32_t)(rowc * 4 * a.pitch + 12 * bxc);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint3 v = *reinterpret_cast<const uint3*>(f + (size_t)i * a.pitch);
+            const uint3 v = *reinterpret_cast<const uint3*>(f + (o + (uint32_t)(i * a.pitch)));
             b.px[i][0] = v.x;
             b.px[i][1] = v.y;
             b.px[i][2] = v.z;
@@ -1393,43 +1402,42 @@ __device__ __forceinline__ void fix4_load(const BackArgs& a, int t, int row, int
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int y = 4 * rowc + i;
-            const uint32_t y4 = *reinterpret_cast<const uint32_t*>(f + (size_t)y * a.pitch + xq);
-            const uint8_t* cr = f + a.sf.uoff + (size_t)(y >> 1) * a.sf.cpitch + (FMT == DVC_FMT_NV12 ? xq : xq / 2);
+            const uint32_t y4 = *reinterpret_cast<const uint32_t*>(f + (uint32_t)(y * a.pitch + xq));
+            const uint32_t cr = (uint32_t)(a.sf.uoff + (size_t)(y >> 1) * a.sf.cpitch + (FMT == DVC_FMT_NV12 ? xq : xq / 2));
             uint32_t c1, c2 = 0;
             if constexpr (FMT == DVC_FMT_NV12) {
-                c1 = *reinterpret_cast<const uint32_t*>(cr);
+                c1 = *reinterpret_cast<const uint32_t*>(f + cr);
             } else {
-                c1 = *reinterpret_cast<const uint16_t*>(cr);
-                c2 = *reinterpret_cast<const uint16_t*>(cr + (a.sf.voff - a.sf.uoff));
+                c1 = *reinterpret_cast<const uint16_t*>(f + cr);
+                c2 = *reinterpret_cast<const uint16_t*>(f + (cr + (uint32_t)(a.sf.voff - a.sf.uoff)));
             }
             quad_bgr<FMT>(y4, c1, c2, b.px[i]);
         }
     }
-    b.rf = a.overlay ? reinterpret_cast<const uint16_t*>(a.rblk)[(size_t)t * a.NBY * a.NBX + (size_t)rowc * a.NBX + bxc]
+    b.rf = a.overlay ? *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(a.rblk) +
+                                                           (size_t)t * a.NBY * a.NBX * 2 + (uint32_t)(rowc * a.NBX + bxc) * 2u)
                      : (uint16_t)0;
 }
 
 __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, int bx, const Fix4& b)
 {
-    const size_t o = (size_t)t * a.ostride + (size_t)(row * 4) * a.opitch + 12 * (size_t)bx;
+    const size_t fo = (size_t)t * a.ostride;                            // wave-uniform
+    const uint32_t o = (uint32_t)(row * 4 * a.opitch + 12 * bx);         // per lane
     if (a.overlay && b.rf) {   // (0, 0, 255) where acc > 127; other blocks keep the speculative copy
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            uint8_t ob[12];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool r = (b.rf >> (4 * i + j)) & 1u;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const int bi = 3 * j + c;
-                    ob[bi] = r ? (c == 2 ? 255 : 0) : (uint8_t)((b.px[i][bi >> 2] >> (8 * (bi & 3))) & 255);
-                }
-            }
+            // byte j of M = 0xFF where pixel j's acc > 127 (the four bits spread
+            // to bytes by one carry-free multiply), then the row's 12 bytes as
+            // per-channel masks: B G R B | G R B G | R B G R
+            const uint32_t r4 = (b.rf >> (4 * i)) & 15u;
+            const uint32_t M = ((r4 * 0x00204081u) & 0x01010101u) * 0xFFu;
+            const uint32_t m[3] = {__builtin_amdgcn_perm(M, M, 0x01000000u), __builtin_amdgcn_perm(M, M, 0x02020101u),
+                                   __builtin_amdgcn_perm(M, M, 0x03030302u)};
+            constexpr uint32_t red[3] = {0x00FF0000u, 0x0000FF00u, 0xFF0000FFu};   // (0, 0, 255) per pixel
             uint32_t ow[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d)
-                ow[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-            store_row<3>(a.overlay + o + (size_t)i * a.opitch, ow, 0);
+            for (int d = 0; d < 3; ++d) ow[d] = ((red[d] ^ b.px[i][d]) & m[d]) ^ b.px[i][d];
+            store_row<3>(a.overlay + fo + (o + (uint32_t)(i * a.opitch)), ow, 0);
         }
     }
     if (a.compressed) {   // not static: the YCrCb -> BGR round trip of every pixel
@@ -1452,7 +1460,7 @@ __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, in
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 cw[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-            store_row<3>(a.compressed + o + (size_t)i * a.opitch, cw, 0);
+            store_row<3>(a.compressed + fo + (o + (uint32_t)(i * a.opitch)), cw, 0);
         }
     }
 }
@@ -1476,7 +1484,9 @@ template <int FMT>
 __global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
 {
     const int lane = threadIdx.x & 63;
-    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    // the wave id through readfirstlane: units (frame t, row0) provably
+    // wave-uniform, so frame bases stay in SGPRs (SGPR-base addressing)
+    const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)), nw = gridDim.x * 4;
     const int SW = a.SW;
     const int ug = (a.NBY + RG - 1) / RG, total = ug * a.n;
     const int fullx = a.g.W / 4, fully = a.g.H / 4;   // full blocks (partial edge blocks: k_out_gen)
