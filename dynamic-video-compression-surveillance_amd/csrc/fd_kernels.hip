@@ -907,6 +907,7 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
     for (int i = 0; i < B; ++i) out[i] = 0;
     // rows four at a time: the 12 loads first (rows not kept read row 0 and
     // are discarded), then the shifts
+    auto ld64 = [&](uint32_t w) { return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(kb) + w * 8u); };
     auto rows = [&](auto big) {   // big: windows past 64 rows test ko per row
         for (int r0 = 0; r0 < R; r0 += 4) {
             uint64_t c[4], pv[4], nv[4];
@@ -916,8 +917,9 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
                 bool keep;
                 if constexpr (decltype(big)::value) keep = r < R && in_img(r) && (!ko || ko[row_of(r)]);
                 else keep = r < R && ((kmask >> r) & 1) != 0;
-                const uint64_t* row = kb + (keep ? (size_t)row_of(r) * WW : 0);
-                const uint64_t c0 = row[wi], p0 = row[wl], n0 = row[wr];
+                // kb (frame t = blockIdx.y) is wave-uniform: 32-bit lane offsets
+                const uint32_t ro = (uint32_t)(keep ? row_of(r) * WW : 0);
+                const uint64_t c0 = ld64(ro + wi), p0 = ld64(ro + wl), n0 = ld64(ro + wr);
                 // the masks pass through an empty asm so that the compiler
                 // cannot turn "keep ? load : 0" back into a branch around the load
                 uint32_t mc = keep ? ~0u : 0u, mp = keep && wi > 0 ? ~0u : 0u, mn = keep && wi + 1 < WW ? ~0u : 0u;
@@ -949,15 +951,16 @@ __global__ void __launch_bounds__(256) k_dilate(BackArgs a)
         for (int i = 0; i < B; ++i)
             if (y0 + i < H) a.dbg_dil[(size_t)(y0 + i) * WW + wi] = out[i];
     }
-    BT* db = reinterpret_cast<BT*>(a.dblk) + (size_t)t * NBY * NBX + (size_t)by * NBX;
+    uint8_t* db = reinterpret_cast<uint8_t*>(a.dblk) + (size_t)t * NBY * NBX * sizeof(BT);   // wave-uniform
     constexpr int PER = 64 / B;
     const int nb = min(PER, NBX - wi * PER);
+    const uint32_t dbo = (uint32_t)(by * NBX + wi * PER) * (uint32_t)sizeof(BT);
 #pragma unroll
     for (int b = 0; b < PER; ++b) {
         uint64_t f = 0;
 #pragma unroll
         for (int i = 0; i < B; ++i) f |= ((out[i] >> (B * b)) & ((1ull << B) - 1)) << (B * i);
-        if (b < nb) db[wi * PER + b] = (BT)f;
+        if (b < nb) *reinterpret_cast<BT*>(db + (dbo + (uint32_t)(b * sizeof(BT)))) = (BT)f;
     }
 }
 
