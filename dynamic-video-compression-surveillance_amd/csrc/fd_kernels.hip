@@ -138,11 +138,14 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 #ifndef DVC_FRONT_WGS_BGR
 #define DVC_FRONT_WGS_BGR 4
 #endif
+#ifndef DVC_FRONT_WGS_PF2   // two frames in flight (the fused BGR default): 119 VGPRs
+#define DVC_FRONT_WGS_PF2 4
+#endif
 #ifndef DVC_FRONT_WGS_YUV
 #define DVC_FRONT_WGS_YUV 5
 #endif
 template <int NW, int PF, int FMT, bool OUT>
-__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : 3) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
@@ -1848,7 +1851,10 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     const int chunk = (n + chunks - 1) / chunks;
     chunks = (n + chunk - 1) / chunk;
     static const int xcd = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : 0; }();
-    static const int pf = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 1; }();
+    // frames in flight per workgroup: the fused BGR front 2 (+1 % against 1 at
+    // 4 workgroups a CU, 119 VGPRs), the others 1; DVC_FRONT_PF overrides
+    static const int pf_env = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 0; }();
+    const int pf = pf_env > 0 ? pf_env : (fo ? 2 : 1);
     const dim3 grid(tx, ty, chunks), block(64 * NW);
     const FrontOut none{};
     if constexpr (NW == 4 || NW == 8) {
