@@ -232,8 +232,15 @@ def lib() -> ctypes.CDLL:
                  "dvc_fd_get_stats", "dvc_fd_read_plane", "dvc_fd_ktime", "dvc_gaussian_taps_q8",
                  "dvc_contour_filter", "dvc_fd_step_batch"):
         getattr(L, name).restype = ctypes.c_int
-    if L.dvc_abi_version() != ABI_VERSION and not os.environ.get("DVC_LIB_PATH"):   # A/B of older builds
-        raise ImportError("libdvc_hip.so ABI version mismatch")
+    if L.dvc_abi_version() != ABI_VERSION:
+        # a library with another dvc_fd_params / flag layout would corrupt
+        # memory: refuse it unless the caller opts in explicitly (A/B of builds
+        # from an older tree whose layout is known to match)
+        if os.environ.get("DVC_ALLOW_ABI_MISMATCH") != "1":
+            raise ImportError(f"{path}: ABI version {L.dvc_abi_version()} != {ABI_VERSION} "
+                              "(set DVC_ALLOW_ABI_MISMATCH=1 to load it anyway)")
+        import warnings
+        warnings.warn(f"{path}: ABI version mismatch accepted (DVC_ALLOW_ABI_MISMATCH=1)")
     _lib = L
     return L
 

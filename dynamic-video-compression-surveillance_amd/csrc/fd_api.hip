@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/dvc.h"
+#include "dct_const.h"
 #include "fd_kernels.h"
 #include "host_common.h"
 #include "yuv_kernels.h"
@@ -69,6 +70,15 @@ void gauss_f64(int n, double sigma, double* k)
 
 void dct_matrix(int B, dvc::DctMat& M)
 {
+    // the fast block sizes take the compiled tables (dct_const.h), so the host
+    // basis and the kernels' constant basis cannot differ on a host whose libm
+    // cos rounds differently
+    if (B == 4 || B == 8) {
+        const float* t = B == 4 ? dvc::kDct4Host : dvc::kDct8Host;
+        std::memcpy(M.m, t, sizeof(float) * B * B);
+        std::memcpy(M.mt, t + B * B, sizeof(float) * B * B);
+        return;
+    }
     const double PI = 3.14159265358979323846;
     for (int k = 0; k < B; ++k)
         for (int n = 0; n < B; ++n) {
@@ -435,6 +445,13 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
             return fail(DVC_E_UNSUPPORTED, "frame width %d: the contour filter's row index needs %zu B of LDS (max %d)",
                         p.width, dvc::ccl_max_lds(h->g), lds);
         }
+        // k_out_gen stages one block's two B x B float planes (+ a flag word)
+        const size_t gen_lds = (size_t)8 * p.block * p.block + 4;
+        if (gen_lds > (size_t)lds) {
+            delete h;
+            return fail(DVC_E_UNSUPPORTED, "block_size %d: the output stage needs %zu B of LDS (max %d)", p.block,
+                        gen_lds, lds);
+        }
     }
     h->gs = (p.width + 3) & ~3;
     h->ip = 3 * h->gs;
@@ -490,9 +507,12 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     for (auto sp : {std::make_pair(&h->s_front, level(prio[0])), std::make_pair(&h->s_acc, level(prio[2])),
                     std::make_pair(&h->s_out, level(prio[3]))})
         if ((e = mk(sp.first, sp.second)) != hipSuccess) return bad(e, "hipStreamCreate");
-    // DVC_CU_SPLIT=k (experiment): the contour filter, accumulate and output /
-    // fix-up streams on k CUs spread evenly over the device, the front on the
-    // others (stream priorities do not apply to CU-masked streams)
+#ifdef DVC_EXPERIMENTS
+    // DVC_CU_SPLIT=k (experiment build only): the contour filter, accumulate
+    // and output / fix-up streams on k CUs spread evenly over the device, the
+    // front on the others. The masked streams are built before the default
+    // ones are released; they are blocking streams without priorities (the
+    // CU-mask API takes neither).
     if (const char* cs = getenv("DVC_CU_SPLIT"); cs && *cs) {
         int ncu = 256;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
@@ -502,14 +522,20 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
             const bool a = (long long)i * k / ncu != (long long)(i + 1) * k / ncu;
             (a ? ma : mb)[i / 32] |= 1u << (i % 32);
         }
-        for (hipStream_t* st : {&h->stream, &h->s_acc, &h->s_front, &h->s_out}) (void)hipStreamDestroy(*st);
         const uint32_t nw = (uint32_t)ma.size() * 32;
-        if ((e = hipExtStreamCreateWithCUMask(&h->stream, nw, ma.data())) != hipSuccess ||
-            (e = hipExtStreamCreateWithCUMask(&h->s_acc, nw, ma.data())) != hipSuccess ||
-            (e = hipExtStreamCreateWithCUMask(&h->s_out, nw, ma.data())) != hipSuccess ||
-            (e = hipExtStreamCreateWithCUMask(&h->s_front, nw, mb.data())) != hipSuccess)
-            return bad(e, "hipExtStreamCreateWithCUMask");
+        hipStream_t ns[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int i = 0; i < 4; ++i)
+            if ((e = hipExtStreamCreateWithCUMask(&ns[i], nw, i < 3 ? ma.data() : mb.data())) != hipSuccess) {
+                for (int k2 = 0; k2 < i; ++k2) (void)hipStreamDestroy(ns[k2]);
+                return bad(e, "hipExtStreamCreateWithCUMask");
+            }
+        hipStream_t* olds[4] = {&h->stream, &h->s_acc, &h->s_out, &h->s_front};
+        for (int i = 0; i < 4; ++i) {
+            (void)hipStreamDestroy(*olds[i]);
+            *olds[i] = ns[i];
+        }
     }
+#endif
     const size_t W = p.width, H = p.height, N = W * H, WW = h->g.WW;
     const size_t nfield = (size_t)h->NBX * h->NBY;   // block fields per frame
     for (int k = 0; k < NSLOT; ++k) {
@@ -783,14 +809,20 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
 {
     Slot& S = h->slot[h->seq % NSLOT];
     hipStream_t s_ccl = h->stream;
+#ifdef DVC_ABLATION
     // DVC_FD_SKIP (stage ablation for profiling only, results are wrong when
-    // set): bit 0 front, 1 contour filter, 2 dilate + accumulate, 3 output
+    // set): bit 0 front, 1 contour filter, 2 dilate + accumulate, 3 output.
+    // Only in the ablation build (tools/build_variant.sh <out> -DDVC_ABLATION),
+    // never in the shipping library.
     static const int skip = [] {
         const char* e = getenv("DVC_FD_SKIP");
         const int v = e ? atoi(e) : 0;
         if (v) std::fprintf(stderr, "dvc: DVC_FD_SKIP=%d set: stages skipped, outputs are wrong (profiling only)\n", v);
         return v;
     }();
+#else
+    constexpr int skip = 0;
+#endif
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
     const uint8_t* d = nullptr;
     int dp = 0;

@@ -1844,8 +1844,11 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
         // 534 k Mpx/s at 1 / 4 / 8 chunks — a warm-up frame per chunk is 2 % more
         // reads, more workgroups in flight hide the per-frame barriers);
         // DVC_FUSED_CHUNKS overrides
+        // at least ~2048 workgroups (8 a CU) when the batch is short: 1080p x 32
+        // frames as one chunk is 544 workgroups, half the device (4 chunks of 8
+        // frames: 299.7 -> 314.4 k Mpx/s at --batch 32, experiments/README.md)
         static const int fc = [] { const char* e = getenv("DVC_FUSED_CHUNKS"); return e ? atoi(e) : 0; }();
-        chunks = fc > 0 ? fc : std::max(1, n / 48);
+        chunks = fc > 0 ? fc : std::max({1, n / 48, (2048 + tx * ty - 1) / (tx * ty)});
     }
     chunks = std::max(1, std::min(chunks, n / minf));
     const int chunk = (n + chunks - 1) / chunks;

@@ -708,15 +708,20 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // overwrites R slots that only flow(i-2) reads; with RB = window + 2 mb the
     // raw bits flow(i) writes are the evictions only vote(i-2) reads
     OfSlot& S = h->slot[h->seq & 1];
+#ifdef DVC_ABLATION
     // DVC_OF_SKIP (stage ablation for profiling only, results are wrong when
     // set): bit 1 flow, 2 vote + mask morphology / rectangles, 3 k_of_out (the
-    // pyramid always runs: the flow kernels index R by the flow)
+    // pyramid always runs: the flow kernels index R by the flow). Only in the
+    // ablation build (tools/build_variant.sh <out> -DDVC_ABLATION).
     static const int skip = [] {
         const char* e = getenv("DVC_OF_SKIP");
         const int v = e ? atoi(e) : 0;
         if (v) std::fprintf(stderr, "dvc: DVC_OF_SKIP=%d set: stages skipped, outputs are wrong (profiling only)\n", v);
         return v;
     }();
+#else
+    constexpr int skip = 0;
+#endif
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_pyr, S.ev_flow, 0));
     // The pyramid of batch i also waits for the flow of batch i-1 (not only
     // i-2, whose R slots it overwrites): a scan launch needs whole CUs (two of

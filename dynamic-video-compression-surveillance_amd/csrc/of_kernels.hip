@@ -1384,6 +1384,355 @@ __global__ void __launch_bounds__(NT, OCC) k_flow_scan(ScanArgs S)
     }
 }
 
+// ------------------------------------------------- scan, pipelined (m == 4) --
+// k_flow_scan2: the same FarnebackUpdateFlow_Blur order as k_flow_scan (the
+// vertical running sums per column, the horizontal running sums per row, both
+// double, OpenCV's order bit for bit), restructured so that the serial work of
+// one strip item overlaps across row blocks instead of waiting at barriers.
+// One 1024-thread workgroup per CU walks one strip (64 columns + the 2m+1 halo
+// columns) of one frame down its row blocks of RB = 12 rows. Interval k (one
+// barrier each) runs four stages of four different blocks side by side:
+//   wave 0 (chain wave):  C(k)    horizontal sums of block k, in place in its sum buffer
+//   M waves, vertical:    V(k+1)  vertical sums of block k+1 -> sum buffer (k+1) % 3
+//   M waves, positions:   G(k+2)  M (FarnebackUpdateMatrices) of the rows block k+2's
+//                                 vertical sums add -> transfer buffer (k+2) % 2
+//   M waves, pixels:      S(k-1)  flow = G^-1 h of block k-1 from sum buffer (k-1) % 3
+// The vertical chain of (column, channel) subtracts M[y-m-1], the value it
+// added 2m+1 rows earlier: each vertical thread keeps those 9 values in
+// registers (a ring whose phase, 12 b mod 9, is a compile-time constant per
+// block), so the transfer buffer holds only the block's new rows and the M
+// ring of k_flow_scan is gone. Sum buffers are laid out [row][channel][column]
+// (74 doubles a line: conflict-free 16-B chain reads and writes), so the chain
+// reads its operands as b128 pairs and issues ~2 instructions a column.
+#ifndef DVC_S2_EXP
+#define DVC_S2_EXP 0   // timing experiments of variant builds only (tools/build_variant.sh -DDVC_S2_EXP=k)
+#endif
+namespace scan2 {
+constexpr int SW = 64, RB = 12, M = 4, HW = 2 * M + 1, NC = SW + HW;
+constexpr int NT = 1024, NMT = NT - 64;
+constexpr int P = 74;                   // doubles per (row, channel) line of a sum buffer
+constexpr int SVB = RB * 5 * P;         // doubles per sum buffer
+constexpr int TR = RB + M;              // rows of a transfer buffer (block 0 takes M rows more)
+constexpr int TB = TR * NC * 5;         // floats per transfer buffer
+constexpr size_t LDS = (size_t)3 * SVB * 8 + (size_t)2 * TB * 4;
+constexpr int NV = NC * 5;              // vertical chains (column, channel)
+constexpr int S0 = NMT - RB * SW;       // first solve thread (one pixel a thread)
+static_assert(NV <= NMT && RB * NC <= NMT && S0 >= 0 && S0 % 64 == 0, "thread roles");
+static_assert(RB * 5 <= 64, "a block's horizontal chains fit one wave");
+static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "16-B lines on distinct banks");
+}  // namespace scan2
+
+// vertical sums of one block for the thread's chain (channel c, column j):
+// rows i of the block add T[tr0 + i] (the transfer row of M[y+m]) and subtract
+// the value added 9 rows earlier (hist slot (PH + i) % 9); vsum to the sum
+// buffer line (i, c) at column j. PH = y0 % 9.
+template <int PH, int I0 = 0, int I1 = scan2::RB>
+__device__ __forceinline__ void scan2_vrows(const float* __restrict__ t, double* __restrict__ sv, float (&hist)[9],
+                                            double& vsum)
+{
+    using namespace scan2;
+    constexpr int G = 3;   // rows whose transfer loads are issued together
+#pragma unroll
+    for (int i0 = I0; i0 < I1; i0 += G) {
+        float fa[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            if (i0 + u < I1) fa[u] = t[(i0 + u) * NC * 5];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int i = i0 + u, s = (PH + i) % HW;
+            if (i < I1) {
+                const float d = fa[u] - hist[s];
+                hist[s] = fa[u];
+                vsum += (double)d;
+                sv[i * 5 * P] = vsum;
+            }
+        }
+    }
+}
+
+// rows [I0, I1) of block b's vertical sums for the chain (vc, vj): t0 = the
+// block's transfer buffer at (column vj, channel vc), svb = its sum buffer at
+// line (0, vc), column vj. Block 0 starts the chain (OpenCV's init) and reads
+// its rows M below the transfer buffer's first (rows 0 .. M-1 are the start).
+template <int I0, int I1>
+__device__ __forceinline__ void scan2_vpart(int b, const float* t0, double* svb, float (&hist)[9], double& vsum)
+{
+    using namespace scan2;
+    if (b == 0) {
+        if constexpr (I0 == 0) {   // M[0] (m+2) (a float product) + M[1..m-1]; the values
+            // subtracted at rows 0..8 are M[max(y-m-1, 0)]
+            vsum = (double)(t0[0] * (float)(M + 2));
+#pragma unroll
+            for (int r = 1; r < M; ++r) vsum += (double)t0[r * NC * 5];
+#pragma unroll
+            for (int y = 0; y < HW; ++y) hist[y] = t0[max(y - M - 1, 0) * NC * 5];
+        }
+        scan2_vrows<0, I0, I1>(t0 + M * NC * 5, svb, hist, vsum);
+    } else {
+        const int ph = (b * RB) % HW;   // 0, 3 or 6
+        if (ph == 0) scan2_vrows<0, I0, I1>(t0, svb, hist, vsum);
+        else if (ph == 3) scan2_vrows<3, I0, I1>(t0, svb, hist, vsum);
+        else scan2_vrows<6, I0, I1>(t0, svb, hist, vsum);
+    }
+}
+
+#ifdef DVC_SCAN2_STAMPS
+__device__ unsigned long long g_scan2_stamps[32 * 96 * 8];
+#define STAMP2(tt, kk, j) do { if (t == 0 && A.lv.w == A.g.W && s < 32 && (kk) + 1 >= 0 && (kk) + 1 < 96) \
+    g_scan2_stamps[(s * 96 + (kk) + 1) * 8 + (j)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP2(tt, kk, j) do {} while (0)
+#endif
+// One role's item loop (CHAIN: wave 0; else the M waves): both take the same
+// items and run the same barriers; split at the top so that no value of one
+// role is live in the other's code.
+template <int SMODE, bool CHAIN>
+__device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float* tb0, int& s_item, int& s_alive)
+{
+    using namespace scan2;
+    const FlowArgs& A = S.f;
+    const OfGeom& g = A.g;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = A.lv.w, h = A.lv.h;
+    const int NB = S.NB;
+    const size_t lvpx = (size_t)w * h;
+    const uint32_t slot_bytes = (uint32_t)NB * 64u * 16u;
+    const int n = A.n;
+    for (int kq = 0; kq < SCAN_Q; ++kq) {
+        const int q = (int)((blockIdx.x + kq) % SCAN_Q);
+        const int total = q < n ? ((n - 1 - q) / SCAN_Q + 1) * S.S : 0;
+        for (;;) {
+            if (tid == 0) {
+                s_item = (int)atomicAdd(S.next + q, 1u);
+                s_alive = 1;
+            }
+            __syncthreads();
+            const int it = s_item;
+            __syncthreads();
+            if (it >= total) break;
+            const int t = q + SCAN_Q * (it / S.S), s = it % S.S;
+            const int X0 = s * SW, X1 = min(X0 + SW, w), CX0 = X0 - M - 1, nx = X1 - X0;
+            const long long a = A.a0 + t;
+            const float* __restrict__ R0 = A.lv.R + (size_t)ring(a - 1, g.RS) * lvpx * 5;
+            const float* __restrict__ R1 = A.lv.R + (size_t)ring(a, g.RS) * lvpx * 5;
+            const float* src = SMODE == 2 ? A.src + (size_t)t * lvpx * 2 : nullptr;
+            float* dst = A.dst ? A.dst + (size_t)t * lvpx * 2 : nullptr;
+            uint32_t* gp_base = S.gpub + (size_t)(t * S.S + s) * (slot_bytes / 4);
+            if constexpr (CHAIN) {
+                // ---------------------------------------------- chain wave
+                __builtin_amdgcn_s_setprio(3);
+                const __amdgpu_buffer_rsrc_t r_mine =
+                    __builtin_amdgcn_make_buffer_rsrc(gp_base, 0, (int)slot_bytes, SCAN_RSRC_W3);
+                const __amdgpu_buffer_rsrc_t r_left = __builtin_amdgcn_make_buffer_rsrc(
+                    s > 0 ? gp_base - slot_bytes / 4 : gp_base, 0, (int)slot_bytes, SCAN_RSRC_W3);
+                const bool act = lane < RB * 5;
+                const int li = act ? lane : RB * 5 - 1;   // lanes 60..63 repeat lane 59 (same values, same words)
+                __syncthreads();   // p0
+                for (int k = -1; k <= NB; ++k) {
+                    if (lane == 0) STAMP2(t, k, 0);
+                    if (k >= 0 && k < NB) {
+                        const int nrow = min(RB, h - k * RB);
+                        double acc = 0.0;
+                        // (lanes 60..63 poll lane 59's slot: they run its chain and
+                        // store the same values to the same words)
+                        if (s > 0 && li < nrow * 5 && !scan_poll(S, r_left, (uint32_t)(k * 64 + li) * 16u, acc))
+                            s_alive = 0;
+                        // line (i, c) of the block's sum buffer; column x' = x - CX0
+                        double* v = sv0 + (size_t)(k % 3) * SVB + (li / 5) * 5 * P + (li % 5) * P;
+                        if (s == 0) {   // OpenCV's start: vsum[0] (m+2) + vsum[1..m-1] (x' = x + m + 1)
+                            acc = v[M + 1] * (double)(M + 2);
+#pragma unroll
+                            for (int x = 1; x < M; ++x) acc += v[x + M + 1];
+                        }
+                        // g[x] = g[x-1] + (V[x'+9] - V[x']), overwriting V[x'] (x' = xl).
+                        // The line as 16-B pairs (pair p = columns 2p, 2p+1) in a
+                        // register window: group gi (columns 8gi .. 8gi+7) reads pairs
+                        // 4gi .. 4gi+8 and prefetches the 4 pairs group gi+2 adds. A
+                        // pair is loaded before any g lands on its columns (g of group
+                        // gi covers pairs 4gi .. 4gi+3, all loaded by then).
+                        if (lane == 0) STAMP2(t, k, 1);
+                        typedef double d2 __attribute__((ext_vector_type(2)));
+                        constexpr int NPAIR = (SW + HW + 1) / 2;   // 37: columns 0 .. 73
+                        d2* v2 = reinterpret_cast<d2*>(v);
+                        d2 win[13];   // pairs 4gi .. 4gi+12 at group gi
+#pragma unroll
+                        for (int pp = 0; pp < 13; ++pp) win[pp] = v2[pp];
+#pragma unroll
+                        for (int gi = 0; gi < SW / 8; ++gi) {
+                            d2 nxt[4];
+                            if (13 + 4 * gi + 3 < NPAIR) {
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) nxt[u] = v2[13 + 4 * gi + u];
+                            }
+                            double gv[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int ch = u + HW;
+                                const double lo = (u & 1) ? win[u >> 1].y : win[u >> 1].x;
+                                const double hi = (ch & 1) ? win[ch >> 1].y : win[ch >> 1].x;
+                                acc += hi - lo;
+                                gv[u] = acc;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) v2[4 * gi + u] = d2{gv[2 * u], gv[2 * u + 1]};
+#pragma unroll
+                            for (int u = 0; u < 9; ++u) win[u] = win[u + 4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) win[9 + u] = nxt[u];
+                        }
+                        if (s + 1 < S.S && act && lane < nrow * 5) {   // state after column 63 (nx == 64 here)
+                            const unsigned long long bits = __builtin_bit_cast(unsigned long long, acc);
+                            const u32x4 qv = slot_tags(S.epoch, (uint32_t)bits, (uint32_t)(bits >> 32));
+                            __builtin_amdgcn_raw_buffer_store_b128(qv, r_mine, (uint32_t)(k * 64 + lane) * 16u, 0,
+                                                                   CPOL_SC1);
+                        }
+                    }
+                    if (lane == 0) STAMP2(t, k, 2);
+                    __syncthreads();
+                    if (lane == 0) STAMP2(t, k, 3);
+                    if (!s_alive) break;   // uniform: read after the barrier
+                }
+                __builtin_amdgcn_s_setprio(0);
+                continue;
+            } else {
+            // -------------------------------------------------- M waves
+            const int mt = tid - 64;
+            // vertical chain of this thread (channel-major: consecutive threads,
+            // consecutive columns of one channel)
+            const bool vth = mt < NV;
+            const int vc = (vth ? mt : 0) / NC, vj = (vth ? mt : 0) - vc * NC;
+            float hist[HW];
+            double vsum = 0.0;
+            // position of this thread in a block's transfer rows: row pr, column pj
+            const int pr = mt / NC, pj = mt - pr * NC;
+            const int px = min(max(CX0 + pj, 0), w - 1);
+            // the rows whose M block b's vertical sums add: y0 + m .. y0 + m + RB - 1
+            auto grow = [&](int b) { return min(b * RB + M + pr, h - 1); };
+            // G(b)'s loads are spread over two intervals: its flow loads in
+            // interval b-4, its R loads in b-3 (interleaved with that interval's
+            // solve and vertical sums, so that the texture unit drains them
+            // while the waves compute), its M into the transfer buffer at the
+            // start of interval b-2
+            // Two position sets in turn (no register copies between them: a copy of
+            // a set whose loads are in flight makes the compiler wait for them):
+            // at interval k, X holds G(k+2) (its R data arrived) and then takes
+            // G(k+4)'s flow loads; Y holds G(k+3)'s flow and takes its R loads.
+            MatPos<1> PA, PB;
+            auto setpos = [&](MatPos<1>& Q, int b) {
+                Q.xs[0] = px;
+                Q.ys[0] = grow(b);
+                Q.ok[0] = pr < RB;
+                Q.off[0] = ((b & 1) * TB) + (pr * NC + pj) * 5;
+            };
+            auto flowld = [&](MatPos<1>& Q, int b) {
+                setpos(Q, b);
+                mat_stage1<1, SMODE>(A, src, Q);
+            };
+            auto ldR0 = [&](MatPos<1>& Q) { ld5(R0 + 5u * (uint32_t)(Q.ys[0] * w + Q.xs[0]), Q.r0[0]); };
+            auto ldR1 = [&](MatPos<1>& Q, int row) {   // row 0 / 1 of the displaced 2 x 2 neighbourhood
+                int x1, y1;
+                float fx, fy;
+                (void)mat_corner(Q.xs[0], Q.ys[0], Q.dx[0], Q.dy[0], w, h, x1, y1, fx, fy);
+                const int x1c = min(max(x1, 0), max(w - 2, 0)), y1c = min(max(y1, 0), max(h - 2, 0));
+#if DVC_S2_EXP == 1   // (timing experiment, wrong results) undisplaced R1 reads
+                ld10(R1 + 5u * (uint32_t)(min(Q.ys[0] + row, h - 1) * w + min(Q.xs[0], w - 2)), Q.pq[0] + 10 * row);
+#elif DVC_S2_EXP == 2   // (timing experiment, wrong results) no R1 reads
+                for (int u = 0; u < 10; ++u) Q.pq[0][10 * row + u] = Q.r0[0][u % 5];
+#else
+                ld10(R1 + 5u * (uint32_t)((y1c + row) * w + x1c), Q.pq[0] + 10 * row);
+#endif
+            };
+            {   // p0: M rows 0 .. RB + M - 1 (clamped) -> transfer buffer 0, two passes
+                flowld(PB, 1);
+                for (int p = mt; p < TR * NC; p += NMT) {
+                    const int r = p / NC, j = p - r * NC;
+                    MatPos<1> Q;
+                    Q.xs[0] = min(max(CX0 + j, 0), w - 1);
+                    Q.ys[0] = min(r, h - 1);
+                    Q.ok[0] = true;
+                    Q.off[0] = p * 5;
+                    mat_stage1<1, SMODE>(A, src, Q);
+                    mat_stage2<1>(A, R0, R1, Q);
+                    mat_stage3<1>(A, Q, tb0);
+                }
+                mat_stage2<1>(A, R0, R1, PB);   // G(1)'s R loads
+                flowld(PA, 2);
+            }
+            __syncthreads();   // p0
+            auto interval = [&](int k, MatPos<1>& X, MatPos<1>& Y) -> bool {
+                if (k + 2 < NB) mat_stage3<1>(A, X, tb0);   // G(k+2) -> transfer buffer (k+2) % 2
+                // G(k+3): R loads this interval. Every load below is issued
+                // unconditionally (positions are clamped, so always valid; past the
+                // last block they are simply unused): a load under a branch makes
+                // the compiler wait for it where the branch joins.
+                ldR0(Y);
+                __builtin_amdgcn_sched_barrier(0);
+                // S(k-1): one pixel a thread on threads S0 .. NMT-1 (a wave = one row)
+                if (k >= 1 && mt >= S0) {
+                    const int b = k - 1, y0 = b * RB, nrow = min(RB, h - y0);
+                    const int e = mt - S0, i = e >> 6, xl = e & 63;
+                    const double* gg = sv0 + (size_t)(b % 3) * SVB + i * 5 * P + xl;
+                    const double g11 = gg[0] * g.box_scale, g12 = gg[P] * g.box_scale, g22 = gg[2 * P] * g.box_scale;
+                    const double h1 = gg[3 * P] * g.box_scale, h2 = gg[4 * P] * g.box_scale;
+                    const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+                    const float fx = (float)((g11 * h2 - g12 * h1) * idet);
+                    const float fy = (float)((g22 * h1 - g12 * h2) * idet);
+                    const int y = y0 + i, x = X0 + xl;
+                    const bool act = i < nrow && xl < nx;
+                    if (!A.last) {
+                        if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fx, fy);
+                    } else {
+                        const float fxo = act ? fx : 0.f, fyo = act ? fy : 0.f;
+                        const float mag = sqrtf(fxo * fxo + fyo * fyo);   // of:82-83
+                        const unsigned long long word = __ballot(act && mag > g.flow_thr);
+                        uint64_t* mr = A.mring + (size_t)ring(a, g.RB) * h * g.WW;
+                        if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
+                        if (A.dbg_flow && t == A.n - 1 && act)
+                            *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fx, fy);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                ldR1(Y, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                // V(k+1), rows 0..5 / R row 1 / rows 6..11
+                const int vb = k + 1;
+                const float* t0 = tb0 + (size_t)(vb & 1) * TB + vj * 5 + vc;
+                double* svb = sv0 + (size_t)(vb % 3) * SVB + vc * P + vj;
+                if (DVC_S2_EXP != 3 && vth && vb < NB) scan2_vpart<0, RB / 2>(vb, t0, svb, hist, vsum);
+                __builtin_amdgcn_sched_barrier(0);
+                ldR1(Y, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                if (DVC_S2_EXP != 3 && vth && vb < NB) scan2_vpart<RB / 2, RB>(vb, t0, svb, hist, vsum);
+                flowld(X, k + 4);
+                if (tid == 64) STAMP2(t, k, 4);      // arrival at the barrier: V + G wave
+                if (tid == 256) STAMP2(t, k, 5);     // V + G + S wave
+                if (tid == 640) STAMP2(t, k, 6);     // G + S wave
+                if (tid == 1023) STAMP2(t, k, 7);    // S wave (G idle)
+                __syncthreads();
+                return s_alive != 0;
+            };
+            // k = -1: X = G(1)'s set (PB), Y = G(2)'s (PA)
+            for (int k = -1; k <= NB; k += 2) {
+                if (!interval(k, PB, PA)) break;
+                if (k + 1 > NB || !interval(k + 1, PA, PB)) break;
+            }
+            }
+        }
+    }
+}
+
+template <int SMODE>
+__global__ void __launch_bounds__(1024, 1) k_flow_scan2(ScanArgs S)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds_s2[];
+    double* sv0 = lds_s2;                                             // 3 sum buffers
+    float* tb0 = reinterpret_cast<float*>(lds_s2 + 3 * scan2::SVB);   // 2 transfer buffers
+    __shared__ int s_item, s_alive;
+    if (threadIdx.x < 64) scan2_role<SMODE, true>(S, sv0, tb0, s_item, s_alive);
+    else scan2_role<SMODE, false>(S, sv0, tb0, s_item, s_alive);
+}
+
 // -------------------------------------------------------------------- vote --
 // of:84-86: count of the last L = min(frames, window) raw masks (the deque),
 // smoothed = count >= vthr[L]. One lane per 16 px (a u16 of a mask word), the
@@ -2161,6 +2510,21 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                     S.f.src_mode = 2;
                     S.f.src = up;
                 }
+                // the pipelined scan for the reference's winsize 9 (m == 4);
+                // DVC_OF_SCAN2=1 selects it (work in progress: slower than k_flow_scan so far)
+                static const int scan2_env = [] { const char* e = getenv("DVC_OF_SCAN2"); return e ? atoi(e) : 0; }();
+                if (g.m == scan2::M && rb == scan2::RB && scan2_env) {
+                    const int items = S.S * n, grid_s = std::max(1, std::min(items, cus));
+                    if (S.f.src_mode == 2)
+                        hipLaunchKernelGGL(k_flow_scan2<2>, dim3(grid_s), dim3(scan2::NT), scan2::LDS, s, S);
+                    else
+                        hipLaunchKernelGGL(k_flow_scan2<0>, dim3(grid_s), dim3(scan2::NT), scan2::LDS, s, S);
+                    if (ev_it0 && k == k_lo && it == 0) {
+                        const hipError_t e = hipEventRecord(ev_it0, s);
+                        if (e != hipSuccess) return e;
+                    }
+                    continue;
+                }
                 const size_t lds_b = scan_lds_bytes(sw, rb, g.m);
                 const int per_cu = std::max(1, std::min(8, (int)(160 * 1024 / lds_b)));
                 const int items = S.S * n, grid_s = std::max(1, std::min(items, per_cu * cus));
@@ -2231,6 +2595,12 @@ hipError_t of_launch_out(const OfGeom& g, const OfBufs& b, const OfOutArgs& o, i
 
 }  // namespace dvc
 
+#ifdef DVC_SCAN2_STAMPS
+extern "C" int dvc_debug_scan2_stamps(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dvc::g_scan2_stamps), sizeof(dvc::g_scan2_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef DVC_SCAN_STAMPS
 extern "C" int dvc_debug_scan_stamps(unsigned long long* host)
 {

@@ -334,6 +334,22 @@ def test_fd_parity_geometry(gpu_lib, oracle_lib, W, H, n, kw):
     _run_pair(gpu_lib, oracle_lib, clip(W, H, n, seed=W + H, n_objects=4), **kw)
 
 
+@pytest.mark.parametrize("block", [4, 8])
+@pytest.mark.parametrize("ksize", [64, 100, 127])
+def test_fd_parity_large_dilation_fast_blocks(gpu_lib, oracle_lib, block, ksize):
+    """k_dilate<4/8> with windows taller than 64 rows (its rows(std::true_type)
+    branch: kernel_size above ~61 at b=4, ~57 at b=8), fd:106. One small moving
+    object in a tall frame leaves most kept-mask rows empty (sparse kocc), and
+    a second one touching the left/top edges puts the window across the frame
+    border."""
+    from dvc_amd.synthetic import clip
+    frames = clip(320, 400, 7, seed=block * 131 + ksize, n_objects=1)
+    frames[:, :40, :48] = frames[:, :1, :1]          # a flat corner ...
+    for t in range(len(frames)):                     # ... with an object sliding along the edges
+        frames[t, :24 + 3 * t, :20 + 4 * t] = (30 + 20 * t) % 256
+    _run_pair(gpu_lib, oracle_lib, frames, block_size=block, kernel_size=ksize, min_area=30)
+
+
 @pytest.mark.parametrize("SW,SH,W,H,kw", [
     (1920, 1080, 960, 540, dict(block_size=8, kernel_size=10, release_factor=0.3)),   # fd:200-207
     (640, 360, 448, 252, {}),                   # scale 0.7: INTER_LINEAR fixed point

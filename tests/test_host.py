@@ -26,6 +26,17 @@ def test_abi_exports_every_declared_symbol():
     assert L.dvc_abi_version() == dvc_amd._native.ABI_VERSION
 
 
+def test_shipping_library_has_no_result_changing_knobs():
+    """The stage-skip ablations (outputs wrong by design) and the CU-split
+    experiment live only in variant builds (tools/build_variant.sh
+    -DDVC_ABLATION / -DDVC_EXPERIMENTS), never in the default libdvc_hip.so."""
+    import dvc_amd
+    path = dvc_amd._native.build()
+    blob = open(path, "rb").read()
+    for knob in (b"DVC_FD_SKIP", b"DVC_OF_SKIP", b"DVC_CU_SPLIT"):
+        assert knob not in blob, knob
+
+
 def test_abi_gaussian_taps_host_only():
     """dvc_gaussian_taps_q8 is pure host code: same taps as the oracle."""
     import dvc_amd

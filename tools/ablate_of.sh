@@ -4,6 +4,12 @@
 # bench config.   tools/ablate_of.sh [rounds]
 set -e
 cd "$(dirname "$0")/.."
+# The skip masks exist only in the ablation build (the shipping library has
+# no result-changing knobs): build it first, on the CPU side, with
+#   tools/build_variant.sh build/libdvc_ablation.so -DDVC_ABLATION
+ABL=${ABL:-build/libdvc_ablation.so}
+[ -f "$ABL" ] || { echo "missing $ABL (tools/build_variant.sh $ABL -DDVC_ABLATION)"; exit 1; }
+export DVC_LIB_PATH=$ABL
 R=${1:-2}
 OUT=gpurun_out/ablate_of
 mkdir -p $OUT

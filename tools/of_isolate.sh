@@ -4,6 +4,12 @@
 # pyramid and the flow), kernel-trace stats under gpurun_out/of_isolate/.
 set -e
 cd "$(dirname "$0")/.."
+# The skip masks exist only in the ablation build (the shipping library has
+# no result-changing knobs): build it first, on the CPU side, with
+#   tools/build_variant.sh build/libdvc_ablation.so -DDVC_ABLATION
+ABL=${ABL:-build/libdvc_ablation.so}
+[ -f "$ABL" ] || { echo "missing $ABL (tools/build_variant.sh $ABL -DDVC_ABLATION)"; exit 1; }
+export DVC_LIB_PATH=$ABL
 OUT=gpurun_out/of_isolate
 mkdir -p $OUT
 export TMPDIR=/tmp

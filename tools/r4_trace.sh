@@ -1,6 +1,12 @@
 #!/bin/bash
 # GPU box: kernel trace of the fused pipeline + stage ablations (DVC_FD_SKIP).
 cd "$(dirname "$0")/.."
+# The skip masks exist only in the ablation build (the shipping library has
+# no result-changing knobs): build it first, on the CPU side, with
+#   tools/build_variant.sh build/libdvc_ablation.so -DDVC_ABLATION
+ABL=${ABL:-build/libdvc_ablation.so}
+[ -f "$ABL" ] || { echo "missing $ABL (tools/build_variant.sh $ABL -DDVC_ABLATION)"; exit 1; }
+export DVC_LIB_PATH=$ABL
 mkdir -p gpurun_out/tr
 export TMPDIR=/tmp
 A="--steps 20 --warmup 3 --runs 1 --ktime-seconds 1"
