@@ -29,9 +29,11 @@ bracketed by a barrier and a device sync; ``value`` is the median run (max over
 ranks per run), every run's value under ``timing``. ``ranks`` records the
 world size the process group saw and every rank's own frame count.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (k_out: hipEvent time
-per launch on the back stream, in a second pass of the same steps; ``copy``:
-the same bytes against this box's hand-written copy rate, dvc_copy_rate) and
+Extra JSON fields: ``roofline`` for the dominant kernel (the fused k_front:
+hipEvent time per launch on the front stream where it runs, in a second pass of
+the same steps; k_out on the back stream when the one-pass output stage runs —
+block sizes other than 4, I420 outputs; ``copy``: the same bytes against this
+box's hand-written copy rate, dvc_copy_rate) and
 ``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
 feed, with ``all_cores``: one feed per available core up to the box's CPU
 share; rank 0 at N=1 only).
@@ -39,7 +41,8 @@ share; rank 0 at N=1 only).
 ``--path of`` runs the fused optical-flow worker of motion_compression_opt.py
 (of:65-101 + of:141-185: gray, Farneback 3-level pyramid, vote, close/open,
 rectangles, 8x8 three-channel compression) on the same device-resident
-sequence; its dominant kernel is k_flow at pyramid level 0.
+sequence; its dominant kernel is k_flow_scan at pyramid level 0 (OpenCV's
+running box sums, a latency-bound recurrence: roofline on the VALU axis).
 """
 from __future__ import annotations
 
@@ -55,7 +58,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/s (frames/s × H×W) 1080p frame-diff path @1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# k_out (the dominant HBM kernel) algorithmic bytes per pixel per frame: read BGR 3 +
+# fused k_front / k_out (the dominant HBM kernel) algorithmic bytes per pixel per frame: read BGR 3 +
 # acc>127 bit 1/8 (+ one static bit per block, negligible), write overlay 3 + compressed 3
 BACK_BYTES_PER_PX_FRAME = 9.125
 BACK_BYTES_PER_PX_LAUNCH = 0

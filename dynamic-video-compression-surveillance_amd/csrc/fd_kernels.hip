@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(256) k_vblur_q8(const uint32_t* __restrict__ t
 // workgroups in flight for one extra frame read per chunk.
 constexpr int FT_W = 256, FT_Q = FT_W / 4 + 2;
 
+
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <numeric>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 
@@ -48,13 +49,20 @@ namespace dvc {
 // the address rate (TA), not the bytes, bounds the M gathers.
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+#if defined(DVC_S2_EXP) && DVC_S2_EXP == 4   // (timing experiment, wrong results) 16-B aligned R loads
+#define DVC_ALIGN_R(p) reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15)
+#else
+#define DVC_ALIGN_R(p) (p)
+#endif
 __device__ __forceinline__ void ld5(const float* p, float* o)
 {
+    p = DVC_ALIGN_R(p);
     const f4u a = *reinterpret_cast<const f4u*>(p);
     o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = p[4];
 }
 __device__ __forceinline__ void ld10(const float* p, float* o)
 {
+    p = DVC_ALIGN_R(p);
     const f4u a = *reinterpret_cast<const f4u*>(p), b = *reinterpret_cast<const f4u*>(p + 4);
     const f2u c = *reinterpret_cast<const f2u*>(p + 8);
     o[0] = a.x, o[1] = a.y, o[2] = a.z, o[3] = a.w, o[4] = b.x, o[5] = b.y, o[6] = b.z, o[7] = b.w, o[8] = c.x,
@@ -1416,7 +1424,11 @@ constexpr int TR = RB + M;              // rows of a transfer buffer (block 0 ta
 constexpr int TB = TR * NC * 5;         // floats per transfer buffer
 constexpr size_t LDS = (size_t)3 * SVB * 8 + (size_t)2 * TB * 4;
 constexpr int NV = NC * 5;              // vertical chains (column, channel)
-constexpr int S0 = NMT - RB * SW;       // first solve thread (one pixel a thread)
+#ifndef DVC_S2_SPX
+#define DVC_S2_SPX 2
+#endif
+constexpr int SPX = DVC_S2_SPX;         // solve pixels a thread: rows (SPX r .. SPX r + SPX-1) of a wave's 64 columns
+constexpr int S0 = NMT - RB * SW / SPX; // first solve thread
 static_assert(NV <= NMT && RB * NC <= NMT && S0 >= 0 && S0 % 64 == 0, "thread roles");
 static_assert(RB * 5 <= 64, "a block's horizontal chains fit one wave");
 static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "16-B lines on distinct banks");
@@ -1426,29 +1438,42 @@ static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "
 // rows i of the block add T[tr0 + i] (the transfer row of M[y+m]) and subtract
 // the value added 9 rows earlier (hist slot (PH + i) % 9); vsum to the sum
 // buffer line (i, c) at column j. PH = y0 % 9.
-template <int PH, int I0 = 0, int I1 = scan2::RB>
-__device__ __forceinline__ void scan2_vrows(const float* __restrict__ t, double* __restrict__ sv, float (&hist)[9],
-                                            double& vsum)
+// the 9 values a vertical chain subtracts next: a vector value (constant
+// element indices only), so it stays in registers (a float[9] passed by
+// reference went to scratch memory)
+typedef float Hist9 __attribute__((ext_vector_type(16)));
+
+// row I of a block at ring phase PH (y0 % 9 == PH), then the rows after it up
+// to I1: rows are loaded in groups of 3 (the group's LDS reads issued together)
+template <int PH, int I, int I1>
+__device__ __forceinline__ void scan2_vrows_from(const float* __restrict__ t, double* __restrict__ sv, Hist9& hist,
+                                                 double& vsum)
 {
     using namespace scan2;
-    constexpr int G = 3;   // rows whose transfer loads are issued together
+    if constexpr (I < I1) {
+        constexpr int N = (I1 - I) < 3 ? (I1 - I) : 3;
+        float fa[3];
 #pragma unroll
-    for (int i0 = I0; i0 < I1; i0 += G) {
-        float fa[G];
-#pragma unroll
-        for (int u = 0; u < G; ++u)
-            if (i0 + u < I1) fa[u] = t[(i0 + u) * NC * 5];
-#pragma unroll
-        for (int u = 0; u < G; ++u) {
-            const int i = i0 + u, s = (PH + i) % HW;
-            if (i < I1) {
-                const float d = fa[u] - hist[s];
-                hist[s] = fa[u];
-                vsum += (double)d;
-                sv[i * 5 * P] = vsum;
-            }
-        }
+        for (int u = 0; u < N; ++u) fa[u] = t[(I + u) * NC * 5];
+        auto row = [&](auto uc) {
+            constexpr int u = decltype(uc)::value, i = I + u, S = (PH + i) % HW;
+            const float d = fa[u] - hist[S];
+            hist[S] = fa[u];
+            vsum += (double)d;
+            sv[i * 5 * P] = vsum;
+        };
+        row(std::integral_constant<int, 0>{});
+        if constexpr (N > 1) row(std::integral_constant<int, 1>{});
+        if constexpr (N > 2) row(std::integral_constant<int, 2>{});
+        scan2_vrows_from<PH, I + N, I1>(t, sv, hist, vsum);
     }
+}
+
+template <int PH, int I0 = 0, int I1 = scan2::RB>
+__device__ __forceinline__ void scan2_vrows(const float* __restrict__ t, double* __restrict__ sv, Hist9& hist,
+                                            double& vsum)
+{
+    scan2_vrows_from<PH, I0, I1>(t, sv, hist, vsum);
 }
 
 // rows [I0, I1) of block b's vertical sums for the chain (vc, vj): t0 = the
@@ -1456,7 +1481,7 @@ __device__ __forceinline__ void scan2_vrows(const float* __restrict__ t, double*
 // line (0, vc), column vj. Block 0 starts the chain (OpenCV's init) and reads
 // its rows M below the transfer buffer's first (rows 0 .. M-1 are the start).
 template <int I0, int I1>
-__device__ __forceinline__ void scan2_vpart(int b, const float* t0, double* svb, float (&hist)[9], double& vsum)
+__device__ __forceinline__ void scan2_vpart(int b, const float* t0, double* svb, Hist9& hist, double& vsum)
 {
     using namespace scan2;
     if (b == 0) {
@@ -1465,8 +1490,12 @@ __device__ __forceinline__ void scan2_vpart(int b, const float* t0, double* svb,
             vsum = (double)(t0[0] * (float)(M + 2));
 #pragma unroll
             for (int r = 1; r < M; ++r) vsum += (double)t0[r * NC * 5];
-#pragma unroll
-            for (int y = 0; y < HW; ++y) hist[y] = t0[max(y - M - 1, 0) * NC * 5];
+            static_assert(M == 4, "the start below is written out for m == 4");
+            const float r0v = t0[0];
+            hist = r0v;                   // rows 0..5 subtract M[0]
+            hist[6] = t0[1 * NC * 5];     // rows 6..8: M[1..3]
+            hist[7] = t0[2 * NC * 5];
+            hist[8] = t0[3 * NC * 5];
         }
         scan2_vrows<0, I0, I1>(t0 + M * NC * 5, svb, hist, vsum);
     } else {
@@ -1602,7 +1631,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
             // consecutive columns of one channel)
             const bool vth = mt < NV;
             const int vc = (vth ? mt : 0) / NC, vj = (vth ? mt : 0) - vc * NC;
-            float hist[HW];
+            Hist9 hist = 0.f;
             double vsum = 0.0;
             // position of this thread in a block's transfer rows: row pr, column pj
             const int pr = mt / NC, pj = mt - pr * NC;
@@ -1668,28 +1697,36 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 // the compiler wait for it where the branch joins.
                 ldR0(Y);
                 __builtin_amdgcn_sched_barrier(0);
-                // S(k-1): one pixel a thread on threads S0 .. NMT-1 (a wave = one row)
+                // S(k-1) on threads S0 .. NMT-1: a wave = SPX rows of 64 columns, the
+                // lane's SPX pixels solved side by side (independent f64 chains)
                 if (k >= 1 && mt >= S0) {
                     const int b = k - 1, y0 = b * RB, nrow = min(RB, h - y0);
-                    const int e = mt - S0, i = e >> 6, xl = e & 63;
-                    const double* gg = sv0 + (size_t)(b % 3) * SVB + i * 5 * P + xl;
-                    const double g11 = gg[0] * g.box_scale, g12 = gg[P] * g.box_scale, g22 = gg[2 * P] * g.box_scale;
-                    const double h1 = gg[3 * P] * g.box_scale, h2 = gg[4 * P] * g.box_scale;
-                    const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
-                    const float fx = (float)((g11 * h2 - g12 * h1) * idet);
-                    const float fy = (float)((g22 * h1 - g12 * h2) * idet);
-                    const int y = y0 + i, x = X0 + xl;
-                    const bool act = i < nrow && xl < nx;
-                    if (!A.last) {
-                        if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fx, fy);
-                    } else {
-                        const float fxo = act ? fx : 0.f, fyo = act ? fy : 0.f;
-                        const float mag = sqrtf(fxo * fxo + fyo * fyo);   // of:82-83
-                        const unsigned long long word = __ballot(act && mag > g.flow_thr);
-                        uint64_t* mr = A.mring + (size_t)ring(a, g.RB) * h * g.WW;
-                        if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
-                        if (A.dbg_flow && t == A.n - 1 && act)
-                            *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fx, fy);
+                    const int e = mt - S0, i0 = (e >> 6) * SPX, xl = e & 63;
+                    float fx[SPX], fy[SPX];
+#pragma unroll
+                    for (int q = 0; q < SPX; ++q) {
+                        const double* gg = sv0 + (size_t)(b % 3) * SVB + (i0 + q) * 5 * P + xl;
+                        const double g11 = gg[0] * g.box_scale, g12 = gg[P] * g.box_scale, g22 = gg[2 * P] * g.box_scale;
+                        const double h1 = gg[3 * P] * g.box_scale, h2 = gg[4 * P] * g.box_scale;
+                        const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+                        fx[q] = (float)((g11 * h2 - g12 * h1) * idet);
+                        fy[q] = (float)((g22 * h1 - g12 * h2) * idet);
+                    }
+#pragma unroll
+                    for (int q = 0; q < SPX; ++q) {
+                        const int i = i0 + q, y = y0 + i, x = X0 + xl;
+                        const bool act = i < nrow && xl < nx;
+                        if (!A.last) {
+                            if (act) *reinterpret_cast<float2*>(dst + 2u * (uint32_t)(y * w + x)) = make_float2(fx[q], fy[q]);
+                        } else {
+                            const float fxo = act ? fx[q] : 0.f, fyo = act ? fy[q] : 0.f;
+                            const float mag = sqrtf(fxo * fxo + fyo * fyo);   // of:82-83
+                            const unsigned long long word = __ballot(act && mag > g.flow_thr);
+                            uint64_t* mr = A.mring + (size_t)ring(a, g.RB) * h * g.WW;
+                            if (lane == 0 && i < nrow) mr[(size_t)y * g.WW + (X0 >> 6)] = word;
+                            if (A.dbg_flow && t == A.n - 1 && act)
+                                *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fx[q], fy[q]);
+                        }
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -2511,8 +2548,8 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                     S.f.src = up;
                 }
                 // the pipelined scan for the reference's winsize 9 (m == 4);
-                // DVC_OF_SCAN2=1 selects it (work in progress: slower than k_flow_scan so far)
-                static const int scan2_env = [] { const char* e = getenv("DVC_OF_SCAN2"); return e ? atoi(e) : 0; }();
+                // DVC_OF_SCAN2=0 selects the barrier-phased k_flow_scan (A/B)
+                static const int scan2_env = [] { const char* e = getenv("DVC_OF_SCAN2"); return e ? atoi(e) : 1; }();
                 if (g.m == scan2::M && rb == scan2::RB && scan2_env) {
                     const int items = S.S * n, grid_s = std::max(1, std::min(items, cus));
                     if (S.f.src_mode == 2)

@@ -40,7 +40,7 @@ rows = {
     "chain: chain": st[:, :, 2] - st[:, :, 1],
     "chain: barrier wait": st[:, :, 3] - st[:, :, 2],
     "wave 1 (V+G) done": st[:, :, 4] - prev3,
-    "wave 4 (V+G+S) done": st[:, :, 5] - prev3,
+    "wave 4 (V+G[+S]) done": st[:, :, 5] - prev3,
     "wave 10 (G+S) done": st[:, :, 6] - prev3,
     "wave 15 (S) done": st[:, :, 7] - prev3,
     "interval": st[:, :, 3] - prev3,
