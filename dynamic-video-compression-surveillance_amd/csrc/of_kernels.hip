@@ -1428,8 +1428,7 @@ constexpr int NV = NC * 5;              // vertical chains (column, channel)
 #define DVC_S2_SPX 2
 #endif
 constexpr int SPX = DVC_S2_SPX;         // solve pixels a thread: rows (SPX r .. SPX r + SPX-1) of a wave's 64 columns
-constexpr int S0 = NMT - RB * SW / SPX; // first solve thread
-static_assert(NV <= NMT && RB * NC <= NMT && S0 >= 0 && S0 % 64 == 0, "thread roles");
+static_assert(NV <= 6 * 64 && RB * NC <= 15 * 64 && RB == 6 * SPX && NT == 16 * 64, "thread roles (k_flow_scan2)");
 static_assert(RB * 5 <= 64, "a block's horizontal chains fit one wave");
 static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "16-B lines on distinct banks");
 }  // namespace scan2
@@ -1627,14 +1626,28 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
             } else {
             // -------------------------------------------------- M waves
             const int mt = tid - 64;
+            // Roles by wave (wv = 1..15). Waves 0, 4, 8, 12 share a SIMD (a
+            // workgroup's waves go to the SIMDs cyclically), so the chain wave's
+            // SIMD mates 4, 8, 12 take the light role (positions only) and the
+            // position slots left over (RB x NC < 15 x 64) fall on wave 12:
+            //   vertical chains + positions:   waves 1, 2, 3, 5, 6, 7
+            //   solve (SPX rows) + positions:  waves 9, 10, 11, 13, 14, 15
+            //   positions only:                waves 4, 8, 12
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+            const bool light = (wv & 3) == 0;
+            const int vslot = wv <= 7 && !light ? wv - 1 - wv / 4 : -1;               // 0..5
+            const int sslot = wv >= 9 && !light ? wv - 9 - (wv >= 13 ? 1 : 0) : -1;   // 0..5
+            const int gslot = light ? 11 + wv / 4 : wv - 1 - wv / 4;                 // 0..14
             // vertical chain of this thread (channel-major: consecutive threads,
             // consecutive columns of one channel)
-            const bool vth = mt < NV;
-            const int vc = (vth ? mt : 0) / NC, vj = (vth ? mt : 0) - vc * NC;
+            const int vidx = vslot * 64 + lane;
+            const bool vth = vslot >= 0 && vidx < NV;
+            const int vc = (vth ? vidx : 0) / NC, vj = (vth ? vidx : 0) - vc * NC;
             Hist9 hist = 0.f;
             double vsum = 0.0;
             // position of this thread in a block's transfer rows: row pr, column pj
-            const int pr = mt / NC, pj = mt - pr * NC;
+            const int gidx = gslot * 64 + lane;
+            const int pr = gidx / NC, pj = gidx - pr * NC;
             const int px = min(max(CX0 + pj, 0), w - 1);
             // the rows whose M block b's vertical sums add: y0 + m .. y0 + m + RB - 1
             auto grow = [&](int b) { return min(b * RB + M + pr, h - 1); };
@@ -1697,11 +1710,11 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 // the compiler wait for it where the branch joins.
                 ldR0(Y);
                 __builtin_amdgcn_sched_barrier(0);
-                // S(k-1) on threads S0 .. NMT-1: a wave = SPX rows of 64 columns, the
+                // S(k-1) on the solve waves: a wave = SPX rows of 64 columns, the
                 // lane's SPX pixels solved side by side (independent f64 chains)
-                if (k >= 1 && mt >= S0) {
+                if (k >= 1 && sslot >= 0) {
                     const int b = k - 1, y0 = b * RB, nrow = min(RB, h - y0);
-                    const int e = mt - S0, i0 = (e >> 6) * SPX, xl = e & 63;
+                    const int i0 = sslot * SPX, xl = lane;
                     float fx[SPX], fy[SPX];
 #pragma unroll
                     for (int q = 0; q < SPX; ++q) {
@@ -1742,10 +1755,10 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 __builtin_amdgcn_sched_barrier(0);
                 if (DVC_S2_EXP != 3 && vth && vb < NB) scan2_vpart<RB / 2, RB>(vb, t0, svb, hist, vsum);
                 flowld(X, k + 4);
-                if (tid == 64) STAMP2(t, k, 4);      // arrival at the barrier: V + G wave
-                if (tid == 256) STAMP2(t, k, 5);     // V + G + S wave
-                if (tid == 640) STAMP2(t, k, 6);     // G + S wave
-                if (tid == 1023) STAMP2(t, k, 7);    // S wave (G idle)
+                if (tid == 64) STAMP2(t, k, 4);      // arrival at the barrier: wave 1 (V + G)
+                if (tid == 256) STAMP2(t, k, 5);     // wave 4 (G, the chain's SIMD)
+                if (tid == 640) STAMP2(t, k, 6);     // wave 10 (S + G)
+                if (tid == 960) STAMP2(t, k, 7);     // wave 15 (S + G)
                 __syncthreads();
                 return s_alive != 0;
             };

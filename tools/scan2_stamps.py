@@ -3,7 +3,8 @@ stamps (debug build with -DDVC_SCAN2_STAMPS, loaded via DVC_LIB_PATH): frame 0
 of the last level-0 launch, every (strip, interval). Chain wave: 0 start, 1
 after the left-strip poll, 2 after the chain, 3 after the barrier. An M-wave
 waves' arrivals at the interval's barrier: 4 wave 1 (vertical sums + M), 5
-wave 4 (vertical sums + M + solve), 6 wave 9 (M + solve), 7 wave 15 (solve)."""
+wave 4 (M only, on the chain's SIMD), 6 wave 10 (solve + M), 7 wave 15
+(solve + M)."""
 import ctypes
 import os
 import sys
@@ -40,9 +41,9 @@ rows = {
     "chain: chain": st[:, :, 2] - st[:, :, 1],
     "chain: barrier wait": st[:, :, 3] - st[:, :, 2],
     "wave 1 (V+G) done": st[:, :, 4] - prev3,
-    "wave 4 (V+G[+S]) done": st[:, :, 5] - prev3,
-    "wave 10 (G+S) done": st[:, :, 6] - prev3,
-    "wave 15 (S) done": st[:, :, 7] - prev3,
+    "wave 4 (G) done": st[:, :, 5] - prev3,
+    "wave 10 (S+G) done": st[:, :, 6] - prev3,
+    "wave 15 (S+G) done": st[:, :, 7] - prev3,
     "interval": st[:, :, 3] - prev3,
 }
 for nm, d in rows.items():
