@@ -170,6 +170,7 @@ struct dvc_fd {
     int sip = 0;         // pitch of staged source frames (host path): 3 * roundup(sw, 4)
     bool resize = false;
     int fmt = DVC_FMT_BGR;  // frame format handed to prime/step (DVC_FMT_*)
+    bool fused8 = false;    // DVC_FD_FUSED8=1 at create: the fused front for block_size 8 (opt-in)
     int crows = 0;          // YUV: luma rows before the chroma planes (device-pointer frames)
     dvc::ResizeTab rt{};
     int B = 4, NBX = 0, NBY = 0, AP = 0;   // block size, blocks (ceil), acc pitch
@@ -460,6 +461,10 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     h->sip = 3 * ((h->sw + 3) & ~3);
     h->resize = h->sw != p.width || h->sh != p.height;
     h->fmt = p.in_format;
+    {   // DVC_FD_FUSED8=1 (read per handle): the fused front for block_size 8 (see enqueue_batch)
+        const char* e = getenv("DVC_FD_FUSED8");
+        h->fused8 = e && atoi(e) != 0;
+    }
     h->ofb = (p.flags & DVC_FLAG_OUT_I420) ? (size_t)p.width * p.height * 3 / 2 : (size_t)p.width * p.height * 3;
     h->crows = p.chroma_rows ? p.chroma_rows : h->sh;
     h->B = p.block;
@@ -837,8 +842,13 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     // surfaces read in place (or staged), BGR outputs in dword rows;
     // DVC_FD_FUSED=0 turns it off (A/B)
     static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
-    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && h->B == 4 && !out_i420 && !obytes &&
-                       (ov || cp) && h->SW <= 64;   // k_fix4 scans a row in one wave
+    // (B = 4: k_fix4 scans a block row's static words in one wave, SW <= 64;
+    // B = 8, opt-in with DVC_FD_FUSED8=1: BGR frames, fixed up by k_out<8>'s
+    // per-block pass. Not the default: the 8x8 DCT at four lanes a block makes
+    // the VALU-bound front the period — 268-270 k against 288 k Mpx/s for the
+    // one-pass k_out<8> at the __main__ kwargs, experiments/README.md)
+    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && !out_i420 && !obytes && (ov || cp) &&
+                       ((h->B == 4 && h->SW <= 64) || (h->B == 8 && h->fused8 && sf.fmt == DVC_FMT_BGR));
     {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
         const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
         S.olo[0] = (uintptr_t)ov;
@@ -870,6 +880,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         fo.quant = h->p.quant;
         fo.qinv = 1.0 / (double)h->p.quant;
         fo.M = h->M;
+        fo.B = h->B;
     }
     // KTIMING: events around the dominant HBM kernel — the fused front on
     // s_front, else k_out on s_out

@@ -170,7 +170,8 @@ struct FrontOut {
     size_t ostride;
     float quant;
     double qinv;
-    DctMat M;          // 4 x 4 basis
+    DctMat M;          // B x B basis
+    int B;             // block size: 4, or 8 (BGR frames in, NW = 4 tiles)
 };
 // frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
 // gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW;

@@ -145,16 +145,103 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 #ifndef DVC_FRONT_WGS_YUV
 #define DVC_FRONT_WGS_YUV 5
 #endif
-template <int NW, int PF, int FMT, bool OUT>
-__global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+// 8x8 blocks of the fused front (OB = 8, the reference's __main__ variant):
+// four lanes per block (lanes 4q..4q+3 of a wave, r = lane & 3 holds rows 2r,
+// 2r+1), the block's intermediate planes in an LDS scratch of 68 floats (8
+// rows of 8; the pad puts the 16 blocks of a wave on distinct banks). The same
+// operation order as block_dct_quant_pk<8> — every output a first product then
+// fmaf in index order, two outputs per v_pk_fma_f32 — so bit-identical to the
+// one-pass k_out<8>; the quad's lanes are in one wave, so LDS hand-offs between
+// the passes need only wave-level ordering.
+constexpr int DCT8_S = 68;
+__device__ __forceinline__ void dct8_quad(float* S, int r, const float (&x)[2][8], float q, double qinv,
+                                          float (&out)[2][8])
+{
+    const DctMat& M = kDct8;
+    // rows: T[i][k] = sum_n X[i][n] M[k][n], i = 2r, 2r+1
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+            const f32x2* mt = reinterpret_cast<const f32x2*>(M.mt + k);   // (M[k][n], M[k+1][n]) at mt[4n]
+            f32x2 t = (f32x2)(x[ii][0]) * mt[0];
+#pragma unroll
+            for (int n = 1; n < 8; ++n) t = __builtin_elementwise_fma((f32x2)(x[ii][n]), mt[n * 4], t);
+            *reinterpret_cast<f32x2*>(S + (2 * r + ii) * 8 + k) = t;
+        }
+    wave_sync_lds();
+    // columns + quantise: X[k][l] = rint(sum_i M[k][i] T[i][l] / q) q, l = 2r, 2r+1
+    f32x2 tc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tc[i] = *reinterpret_cast<const f32x2*>(S + i * 8 + 2 * r);
+    wave_sync_lds();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        f32x2 t = (f32x2)(M.m[k * 8]) * tc[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) t = __builtin_elementwise_fma((f32x2)(M.m[k * 8 + i]), tc[i], t);
+        *reinterpret_cast<f32x2*>(S + k * 8 + 2 * r) =
+            f32x2{__builtin_rintf(div_rn(t.x, qinv)) * q, __builtin_rintf(div_rn(t.y, qinv)) * q};
+    }
+    wave_sync_lds();
+    // inverse rows: T2[k][n] = sum_l X[k][l] M[l][n], k = 2r, 2r+1
+    float xr[2][8];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) xr[ii][l] = S[(2 * r + ii) * 8 + l];
+    wave_sync_lds();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int n = 0; n < 8; n += 2) {
+            const f32x2* mp = reinterpret_cast<const f32x2*>(M.m + n);    // (M[l][n], M[l][n+1]) at mp[4l]
+            f32x2 t = (f32x2)(xr[ii][0]) * mp[0];
+#pragma unroll
+            for (int l = 1; l < 8; ++l) t = __builtin_elementwise_fma((f32x2)(xr[ii][l]), mp[l * 4], t);
+            *reinterpret_cast<f32x2*>(S + (2 * r + ii) * 8 + n) = t;
+        }
+    wave_sync_lds();
+    // inverse columns: out[i][n] = sum_k M[k][i] T2[k][n], i = 2r, 2r+1 (k in order)
+    f32x2 acc[2][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        f32x2 row[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) row[p] = *reinterpret_cast<const f32x2*>(S + k * 8 + 2 * p);
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+            const f32x2 m = (f32x2)(M.m[k * 8 + 2 * r + ii]);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) acc[ii][p] = k == 0 ? m * row[p] : __builtin_elementwise_fma(m, row[p], acc[ii][p]);
+        }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            out[ii][2 * p] = acc[ii][p].x;
+            out[ii][2 * p + 1] = acc[ii][p].y;
+        }
+    wave_sync_lds();   // the scratch is rewritten by the next frame
+}
+
+#ifndef DVC_FRONT_WGS_B8   // fused 8x8 blocks: 3 workgroups a CU (4 spill 20 VGPRs)
+#define DVC_FRONT_WGS_B8 3
+#endif
+template <int NW, int PF, int FMT, bool OUT, int OB = 4>
+__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
 {
     static_assert(!OUT || NW == 4 || NW == 8, "fused outputs: 16- or 32-row tiles");
+    static_assert(!OUT || OB == 4 || (OB == 8 && NW == 4), "fused 8x8 blocks: 16-row tiles (64 blocks, 4 lanes each)");
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
+    constexpr bool B8 = OUT && OB == 8;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
     __shared__ uint2 sh[FT_R][FT_W / 4];       // horizontal Q8 sums, 4 x u16 per quad
+    __shared__ __attribute__((aligned(16))) float s8[B8 ? 64 * DCT8_S : 1];   // OB = 8: the blocks' DCT planes
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // LDS row of this wave's j-th loaded row, and tile row of its i-th output row
     // (OUT: the 4 halo rows 0, 1, FT_H + 2, FT_H + 3 go to waves 0..3; a wave
@@ -274,7 +361,17 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR 
     constexpr uint32_t K5 = 1u | (4u << 8) | (6u << 16) | (4u << 24);
     // OUT: this lane's block lies inside the frame (partial edge blocks are
     // k_out_gen's) and the frame is one of the chunk's (not its warm-up)
-    const bool full_blk = OUT && x + 4 <= W && y0 + 4 * wave + 4 <= H;
+    // (OB = 8: the lane's 4x4 quarter lies in a full 8x8 block)
+    const bool full_blk = OUT && (OB == 8 ? (x & ~7) + 8 <= W && ((y0 + 4 * wave) & ~7) + 8 <= H
+                                          : x + 4 <= W && y0 + 4 * wave + 4 <= H);
+    // OB = 8: this thread's quarter of block q8 (32 x 2 blocks a tile): rows 2 r8,
+    // 2 r8 + 1; the block's compressed rows go out from these lanes
+    const int q8 = threadIdx.x >> 2, r8 = threadIdx.x & 3, bx8 = q8 & 31, by8 = q8 >> 5;
+    const bool full8 = B8 && x0 + 8 * bx8 + 8 <= W && y0 + 8 * by8 + 8 <= H;
+    uint32_t o8[2];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+        o8[ii] = B8 ? (uint32_t)((size_t)(y0 + 8 * by8 + 2 * r8 + ii) * fo.opitch + 3 * (size_t)(x0 + 8 * bx8)) : 0u;
     // OUT rows and motion-bit words: per-lane 32-bit offsets from the frame's
     // wave-uniform base (through voff once per frame, like the loads)
     uint32_t oro[4], mwo[4];
@@ -288,6 +385,10 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR 
         for (int i = 0; i < 4; ++i) {
             if constexpr (OUT) oro[i] = voff(oro[i]);
             mwo[i] = voff(mwo[i]);
+        }
+        if constexpr (B8) {
+            o8[0] = voff(o8[0]);
+            o8[1] = voff(o8[1]);
         }
         // OUT: the block's 4 rows as BGR (4:2:0 surfaces converted once, for
         // both the gray and the overlay); other rows straight to gray
@@ -344,13 +445,50 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR 
             }
         }
         __syncthreads();
+        if constexpr (B8) {
+            // OB = 8: the compressed blocks, before the next frame's loads are
+            // issued (their registers are free here; sg holds this frame until
+            // the next barrier). Every lane runs its block's passes (the
+            // wave-level LDS ordering needs the whole quad); only full blocks
+            // are stored
+            if (fo.cp && t >= t_first) {
+                float xg[2][8], yo[2][8];
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {   // rows 2 r8, 2 r8 + 1 of block q8: two quads each
+                        const uint32_t gw = sg[2 + 8 * by8 + 2 * r8 + ii][1 + 2 * bx8 + jj];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) xg[ii][4 * jj + j] = (float)((int)((gw >> (8 * j)) & 255u) - 128);
+                    }
+                dct8_quad(s8 + q8 * DCT8_S, r8, xg, fo.quant, fo.qinv, yo);
+                if (full8) {
+                    uint8_t* o = fo.cp + (size_t)t * fo.ostride;
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii) {
+                        uint32_t cw[6];
+#pragma unroll
+                        for (int h4 = 0; h4 < 2; ++h4) {
+                            uint32_t u[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)   // clip to [0, 255], truncating uint8 cast
+                                u[j] = (uint32_t)__builtin_amdgcn_fmed3f(yo[ii][4 * h4 + j] + 128.0f, 0.0f, 255.0f);
+                            gray_bgr4(u[0], u[1], u[2], u[3], &cw[3 * h4]);
+                        }
+                        uint32_t* r = reinterpret_cast<uint32_t*>(o + o8[ii]);
+#pragma unroll
+                        for (int d = 0; d < 6; ++d) __builtin_nontemporal_store(cw[d], r + d);
+                    }
+                }
+            }
+        }
         // frame t + PF into the set just converted (the last frames reload
         // themselves: an unconditional load)
         load(qs, bgr + (size_t)min(t + PF, t_end - 1) * fstride);
         // OUT: the block's gray quads (this frame's sg is rewritten only after
         // the barrier below)
         uint32_t gq[4];
-        if constexpr (OUT) {
+        if constexpr (OUT && !B8) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) gq[i] = sg[2 + 4 * wave + i][lane + 1];
         }
@@ -413,7 +551,7 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (PF == 1 ? (FMT == DVC_FMT_BGR 
         }
         // OUT: compressed := the block as static (fd:117-130): Y' = trunc(clip(
         // IDCT(rint(DCT(Y - 128) / q) q) + 128)), Cr = Cb = 128 -> (Y', Y', Y')
-        if constexpr (OUT) {
+        if constexpr (OUT && !B8) {
             if (fo.cp && full_blk && t >= t_first) {
                 float X[16];
 #pragma unroll
@@ -1870,6 +2008,13 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
             // DVC_FRONT_LDS=<bytes> (experiment): unused dynamic LDS per workgroup, to
             // cap the fused front's workgroups per CU and leave room to the others
             static const size_t pad = [] { const char* e = getenv("DVC_FRONT_LDS"); return e ? (size_t)atol(e) : 0; }();
+            if constexpr (NW == 4) {
+                if (fo->B == 8) {   // 8x8 blocks (BGR frames; launch_front checked the rest)
+                    hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true, 8>), grid, block, pad, s, bgr, pitch, fstride, sf,
+                                       n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
+                    return;
+                }
+            }
             if (sf.fmt == DVC_FMT_NV12)
                 hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
@@ -1903,11 +2048,13 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const Src
                         uint8_t* gray_out, int gs, uint64_t* mbits, const RowGeom& g, int ithresh, hipStream_t s,
                         const FrontOut* fo)
 {
-    if (fo && !dct4_is_const(fo->M)) return hipErrorInvalidValue;   // the fused DCT's constant basis
+    if (fo && !(fo->B == 4 ? dct4_is_const(fo->M) : fo->B == 8 && dct8_is_const(fo->M)))
+        return hipErrorInvalidValue;   // the fused DCT's constant basis
+    if (fo && fo->B == 8 && sf.fmt != DVC_FMT_BGR) return hipErrorInvalidValue;   // 8x8: BGR frames only
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
     if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
-    else if (nw == 8) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
+    else if (nw == 8 && !(fo && fo->B == 8)) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     return hipGetLastError();
 }
@@ -2071,6 +2218,11 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
     const int ntx = (a.g.W + 64 * B - 1) / (64 * B), nty = (a.g.H + 4 * B - 1) / (4 * B);
     const int grid = std::max(1, std::min(wgs, ntx * nty * a.n));
     const int f = a.sf.fmt;
+    if (fix && B == 8) {   // the fused 8x8 front's fix-up: k_out's per-block pass, non-static blocks only
+        if (a.out_i420 || a.obytes || f != DVC_FMT_BGR) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+        return hipGetLastError();
+    }
     if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR out in dword rows)
         if (B != 4 || a.out_i420 || a.obytes) return hipErrorInvalidValue;
         static const int fwgs = [] {   // DVC_FIX_WGS: k_fix4 workgroups (default 6 per CU: all resident at 79 VGPRs)

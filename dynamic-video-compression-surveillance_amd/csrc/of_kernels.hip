@@ -266,9 +266,14 @@ __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* 
 {
     constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG;
     constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
-    __shared__ __attribute__((aligned(16))) float sg[GH * GW];
+    // sg (gray, read by the blur) and sv (the vertical sums, written after the
+    // blur's barrier) share one array: 22 KB instead of 31 KB a workgroup, six
+    // workgroups a CU instead of five (the 76-VGPR kernel allows six)
+    constexpr int SGV = GH * GW > PT_H * IW * 3 ? GH * GW : PT_H * IW * 3;
+    __shared__ __attribute__((aligned(16))) float sgv[SGV];
     __shared__ float sI[IH * IW];
-    __shared__ float sv[PT_H * IW * 3];
+    float* sg = sgv;
+    float* sv = sgv;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     const bool interior = x0 >= GX && x0 + PT_W + GX <= g.W && y0 >= HG && y0 + PT_H + HG <= g.H;   // uniform
     if (interior) front0_tile<PN, true, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sg, sI, sv);
@@ -850,13 +855,18 @@ __device__ __forceinline__ void mat_stage2(const FlowArgs& A, const float* __res
     }
 }
 
+// Branch-free up to the LDS store: every position's arithmetic runs (positions
+// past the block are valid clamped ones), the out-of-range bilinear case is a
+// select. A branch around the uses of the loaded values would let a whole wave
+// skip them, after which the compiler must treat those loads as still in
+// flight and waits for them at the next write of their registers (inside the
+// scan's solve: s_waitcnt vmcnt in the middle of the division).
 template <int MQ>
-__device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& P, float* sM)
+__device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& P, float* sM, bool store = true)
 {
     const int w = A.lv.w, h = A.lv.h;
 #pragma unroll
     for (int u = 0; u < MQ; ++u) {
-        if (!P.ok[u]) continue;
         const int x = P.xs[u], y = P.ys[u];
         const float dx = P.dx[u], dy = P.dy[u];
         int x1, y1;
@@ -865,24 +875,21 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
         const float* r0 = P.r0[u];
         const float* p = P.pq[u];
         const float* q = P.pq[u] + 10;
-        f32x2 R23, R45;
-        float r6;
         const f32x2 R0_01 = {r0[0], r0[1]}, R0_23 = {r0[2], r0[3]};
-        if (inb) {
-            const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
-            const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
-            const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
-            const f32x2 Q01 = {q[0], q[1]}, Q23 = {q[2], q[3]}, Q56 = {q[5], q[6]}, Q78 = {q[7], q[8]};
-            R23 = A00 * P01 + A01 * P56 + A10 * Q01 + A11 * Q56;
-            R45 = A00 * P23 + A01 * P78 + A10 * Q23 + A11 * Q78;
-            r6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
-            R45 = (R0_23 + R45) * (f32x2)0.5f;
-            r6 = (r0[4] + r6) * 0.25f;
-        } else {
-            R23 = (f32x2)0.f;
-            R45 = R0_23;
-            r6 = r0[4] * 0.5f;
-        }
+        // in range: the bilinear R1 (the oracle's inside branch)
+        const float a00 = (1.f - fx) * (1.f - fy), a01 = fx * (1.f - fy), a10 = (1.f - fx) * fy, a11 = fx * fy;
+        const f32x2 A00 = a00, A01 = a01, A10 = a10, A11 = a11;
+        const f32x2 P01 = {p[0], p[1]}, P23 = {p[2], p[3]}, P56 = {p[5], p[6]}, P78 = {p[7], p[8]};
+        const f32x2 Q01 = {q[0], q[1]}, Q23 = {q[2], q[3]}, Q56 = {q[5], q[6]}, Q78 = {q[7], q[8]};
+        const f32x2 I23 = A00 * P01 + A01 * P56 + A10 * Q01 + A11 * Q56;
+        f32x2 I45 = A00 * P23 + A01 * P78 + A10 * Q23 + A11 * Q78;
+        float i6 = a00 * p[4] + a01 * p[9] + a10 * q[4] + a11 * q[9];
+        I45 = (R0_23 + I45) * (f32x2)0.5f;
+        i6 = (r0[4] + i6) * 0.25f;
+        // out of range: R1 terms zero
+        f32x2 R23 = inb ? I23 : (f32x2)0.f;
+        f32x2 R45 = inb ? I45 : R0_23;
+        float r6 = inb ? i6 : r0[4] * 0.5f;
         R23 = (R0_01 - R23) * (f32x2)0.5f;
         R23 = R23 + ((f32x2){R45.x, r6} * (f32x2)dy + (f32x2){r6, R45.y} * (f32x2)dx);
         if ((unsigned)(x - 5) >= (unsigned)(w - 10) || (unsigned)(y - 5) >= (unsigned)(h - 10)) {
@@ -892,14 +899,17 @@ __device__ __forceinline__ void mat_stage3(const FlowArgs& A, const MatPos<MQ>& 
             R45 = R45 * (f32x2)scale;
             r6 *= scale;
         }
-        float* M = sM + P.off[u];
         const f32x2 G = R45 * R45 + (f32x2)(r6 * r6);
         const f32x2 Hh = (f32x2){R45.x, r6} * (f32x2)R23.x + (f32x2){r6, R45.y} * (f32x2)R23.y;
-        M[0] = G.x;
-        M[1] = (R45.x + R45.y) * r6;
-        M[2] = G.y;
-        M[3] = Hh.x;
-        M[4] = Hh.y;
+        const float m1 = (R45.x + R45.y) * r6;
+        if (store && P.ok[u]) {
+            float* M = sM + P.off[u];
+            M[0] = G.x;
+            M[1] = m1;
+            M[2] = G.y;
+            M[3] = Hh.x;
+            M[4] = Hh.y;
+        }
     }
 }
 
@@ -1587,7 +1597,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
 #pragma unroll
                         for (int pp = 0; pp < 13; ++pp) win[pp] = v2[pp];
 #pragma unroll
-                        for (int gi = 0; gi < SW / 8; ++gi) {
+                        for (int gi = 0; gi < (DVC_S2_EXP == 7 ? 0 : SW / 8); ++gi) {
                             d2 nxt[4];
                             if (13 + 4 * gi + 3 < NPAIR) {
 #pragma unroll
@@ -1703,7 +1713,8 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
             }
             __syncthreads();   // p0
             auto interval = [&](int k, MatPos<1>& X, MatPos<1>& Y) -> bool {
-                if (k + 2 < NB) mat_stage3<1>(A, X, tb0);   // G(k+2) -> transfer buffer (k+2) % 2
+                mat_stage3<1>(A, X, tb0, k + 2 < NB);   // G(k+2) -> transfer buffer (k+2) % 2 (always
+                                                        // computed: the loads are consumed on every path)
                 // G(k+3): R loads this interval. Every load below is issued
                 // unconditionally (positions are clamped, so always valid; past the
                 // last block they are simply unused): a load under a branch makes
@@ -1711,20 +1722,34 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 ldR0(Y);
                 __builtin_amdgcn_sched_barrier(0);
                 // S(k-1) on the solve waves: a wave = SPX rows of 64 columns, the
-                // lane's SPX pixels solved side by side (independent f64 chains)
-                if (k >= 1 && sslot >= 0) {
-                    const int b = k - 1, y0 = b * RB, nrow = min(RB, h - y0);
+                // lane's SPX pixels solved side by side (independent f64 chains);
+                // their stores are issued at the end of the interval, after this
+                // interval's gathers: vmcnt counts loads and stores in one queue,
+                // so a store issued before a load makes the next wait for that
+                // load wait for the store's completion too
+                const bool sdo = k >= 1 && sslot >= 0 && DVC_S2_EXP != 6;
+                float fx[SPX], fy[SPX];
+                if (sdo) {
+                    const int b = k - 1;
                     const int i0 = sslot * SPX, xl = lane;
-                    float fx[SPX], fy[SPX];
 #pragma unroll
                     for (int q = 0; q < SPX; ++q) {
                         const double* gg = sv0 + (size_t)(b % 3) * SVB + (i0 + q) * 5 * P + xl;
                         const double g11 = gg[0] * g.box_scale, g12 = gg[P] * g.box_scale, g22 = gg[2 * P] * g.box_scale;
                         const double h1 = gg[3 * P] * g.box_scale, h2 = gg[4 * P] * g.box_scale;
+#if DVC_S2_EXP == 5   // (timing experiment, wrong results) no division in the solve
+                        const double idet = (g11 * g22 - g12 * g12 + 1e-3) * 0.5;
+#else
                         const double idet = 1. / (g11 * g22 - g12 * g12 + 1e-3);
+#endif
                         fx[q] = (float)((g11 * h2 - g12 * h1) * idet);
                         fy[q] = (float)((g22 * h1 - g12 * h2) * idet);
                     }
+                }
+                auto solve_store = [&]() {
+                    if (!sdo) return;
+                    const int b = k - 1, y0 = b * RB, nrow = min(RB, h - y0);
+                    const int i0 = sslot * SPX, xl = lane;
 #pragma unroll
                     for (int q = 0; q < SPX; ++q) {
                         const int i = i0 + q, y = y0 + i, x = X0 + xl;
@@ -1741,7 +1766,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                                 *reinterpret_cast<float2*>(A.dbg_flow + ((size_t)y * w + x) * 2) = make_float2(fx[q], fy[q]);
                         }
                     }
-                }
+                };
                 __builtin_amdgcn_sched_barrier(0);
                 ldR1(Y, 0);
                 __builtin_amdgcn_sched_barrier(0);
@@ -1755,6 +1780,8 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 __builtin_amdgcn_sched_barrier(0);
                 if (DVC_S2_EXP != 3 && vth && vb < NB) scan2_vpart<RB / 2, RB>(vb, t0, svb, hist, vsum);
                 flowld(X, k + 4);
+                __builtin_amdgcn_sched_barrier(0);
+                solve_store();
                 if (tid == 64) STAMP2(t, k, 4);      // arrival at the barrier: wave 1 (V + G)
                 if (tid == 256) STAMP2(t, k, 5);     // wave 4 (G, the chain's SIMD)
                 if (tid == 640) STAMP2(t, k, 6);     // wave 10 (S + G)

@@ -52,6 +52,65 @@ def test_fused_equals_unfused(gpu_lib, W, H, n, batch, seed, noisy):
         assert torch.equal(cpf[t], cpu_[t]), f"compressed: fused != unfused at frame {t + 1}"
 
 
+@pytest.mark.parametrize("W,H,SW,SH,n,batch,seed,noisy", [
+    (960, 540, 1920, 1080, 33, 16, 11, False),   # fd:200-207: b=8, k=10, r=0.3, scale 0.5 (resized on the GPU)
+    (1920, 1080, 0, 0, 25, 12, 12, True),
+    (652, 364, 0, 0, 31, 10, 13, False),          # partial 8x8 edge blocks: k_out_gen beside the fused front
+    (1000, 200, 0, 0, 21, 20, 14, True),          # tiles past the right edge
+])
+def test_fused_b8_equals_unfused(gpu_lib, W, H, SW, SH, n, batch, seed, noisy, monkeypatch):
+    """block_size 8 (the reference's __main__ variant, fd:200-207): the fused
+    front writes every full 8x8 block as static (4 lanes a block, k_front
+    OB = 8) and k_out<8>'s per-block pass rewrites the non-static ones; every
+    output frame == the one-pass k_out<8> path. (Opt-in: DVC_FD_FUSED8=1 when
+    the handle is created.)"""
+    import torch
+    monkeypatch.setenv("DVC_FD_FUSED8", "1")
+    dev = torch.device("cuda", 0)
+    sw, sh = (SW, SH) if SW else (W, H)
+    _, seq = _frames_dev(sw, sh, n, seed, noisy, dev)
+    kw = dict(block_size=8, kernel_size=10, release_factor=0.3)
+    if SW:
+        kw.update(src_width=SW, src_height=SH)
+    outs = {}
+    for fused in (True, False):
+        w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=batch, fused=fused, ktiming=True, **kw)
+        w.prime(seq[0])
+        ov = torch.empty((n - 1, H, W, 3), dtype=torch.uint8, device=dev)
+        cp = torch.empty_like(ov)
+        w.step_batch(seq[1:], ov, cp)
+        w.sync()
+        assert w.ktime_kernel() == ("k_front_fused" if fused else "k_out")
+        outs[fused] = (ov, cp, w.stats())
+        w.close()
+    (ovf, cpf, sf), (ovu, cpu_, su) = outs[True], outs[False]
+    assert sf == su
+    for t in range(n - 1):
+        assert torch.equal(ovf[t], ovu[t]), f"overlay: fused != unfused at frame {t + 1}"
+        assert torch.equal(cpf[t], cpu_[t]), f"compressed: fused != unfused at frame {t + 1}"
+
+
+def test_fused_b8_matches_oracle(gpu_lib, oracle_lib, monkeypatch):
+    """The fused 8x8 path frame by frame against the CPU oracle (fd:200-207 kwargs)."""
+    from dvc_amd.synthetic import clip
+    monkeypatch.setenv("DVC_FD_FUSED8", "1")
+    W, H, n = 640, 360, 9
+    frames = clip(W, H, n, seed=21, noisy=True)
+    kw = dict(block_size=8, kernel_size=10, release_factor=0.3)
+    gpu = gpu_lib.FDWorker(W, H, **kw)
+    ref = oracle_lib.OracleFD(W, H, **kw)
+    gpu.prime(frames[0])
+    ref.prime(frames[0])
+    for t in range(1, n):
+        ov, cp = gpu.step(frames[t])
+        rov, rcp, _ = ref.step(frames[t])
+        assert np.array_equal(ov, rov), f"overlay differs at frame {t}"
+        assert np.array_equal(cp, rcp), f"compressed differs at frame {t}"
+    assert gpu.stats() == ref.stats()
+    gpu.close()
+    ref.close()
+
+
 def test_fused_one_output(gpu_lib):
     """Only one of the outputs requested: the other pointer is NULL in both kernels."""
     import torch
