@@ -16,10 +16,10 @@ contiguous (2R-2)-frame sequence (FD 1080p: 766 frames, 4.8 GB — far beyond
 the 256 MB Infinity Cache); overlay and compressed outputs go to device buffers
 of the same length. A step = one pass over that sequence through
 dvc_fd_step_batch (launches of --batch frames, FD default 383 at 1080p: larger
-grids keep the latency-bound contour filter occupied and amortise the stage
-hand-offs — interleaved sweeps: 127 → 276 k, 191 → 288 k, 255 → 291 k,
-383 → 298–307 k, 511 → 294 k Mpx/s; --per-frame: one dvc_fd_step per frame
-instead).
+grids keep the latency-bound contour filter occupied and amortise each call's
+fixed serial tail — round 5 on one box: 32 → 296 k, 128 → 349 k, 383 → 368 k
+Mpx/s, profiles/r5_bench_fd_batch*.json; --per-frame: one dvc_fd_step per
+frame instead, 24 k).
 
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
@@ -29,7 +29,7 @@ bracketed by a barrier and a device sync; ``value`` is the median run (max over
 ranks per run), every run's value under ``timing``. ``ranks`` records the
 world size the process group saw and every rank's own frame count.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (the fused k_front:
+Extra JSON fields: ``roofline`` for the dominant kernel (FD: the fused k_front:
 hipEvent time per launch on the front stream where it runs, in a second pass of
 the same steps; k_out on the back stream when the one-pass output stage runs —
 block sizes other than 4, I420 outputs; ``copy``: the same bytes against this
@@ -41,7 +41,7 @@ share; rank 0 at N=1 only).
 ``--path of`` runs the fused optical-flow worker of motion_compression_opt.py
 (of:65-101 + of:141-185: gray, Farneback 3-level pyramid, vote, close/open,
 rectangles, 8x8 three-channel compression) on the same device-resident
-sequence; its dominant kernel is k_flow_scan at pyramid level 0 (OpenCV's
+sequence; its dominant kernel is k_flow_scan2 at pyramid level 0 (OpenCV's
 running box sums, a latency-bound recurrence: roofline on the VALU axis).
 """
 from __future__ import annotations
@@ -432,12 +432,15 @@ def main():
             workload += "_direct_sums"
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
             workload += f"_b{args.block_size}_k{args.kernel_size}_r{args.release_factor:g}"
-        if of:   # kn counts level-0 k_flow launches (iterations per batch)
-            kname = "k_flow"
+        if of:   # kn counts level-0 flow launches (iterations per batch)
+            # the library's level-0 kernel: the pipelined scan unless DVC_OF_SCAN2=0
+            # (the barrier-phased one) or --of-direct (direct per-pixel sums)
+            kname = ("k_flow" if args.of_direct else
+                     "k_flow_scan" if os.environ.get("DVC_OF_SCAN2") == "0" else "k_flow_scan2")
             per_launch_frames = kframes * 2 / max(kn, 1)
             bytes_per_launch = OF_FLOW_BYTES_PER_PX * W * H * per_launch_frames
-            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"),
-                                  "k_flow" if args.of_direct else "k_flow_scan", workload, per_launch_frames)
+            traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"), kname, workload,
+                                  per_launch_frames)
         else:
             kname = kkernel
             per_launch_frames = kframes / max(kn, 1)

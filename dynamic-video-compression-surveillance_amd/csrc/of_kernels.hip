@@ -1434,11 +1434,22 @@ constexpr int TR = RB + M;              // rows of a transfer buffer (block 0 ta
 constexpr int TB = TR * NC * 5;         // floats per transfer buffer
 constexpr size_t LDS = (size_t)3 * SVB * 8 + (size_t)2 * TB * 4;
 constexpr int NV = NC * 5;              // vertical chains (column, channel)
-#ifndef DVC_S2_SPX
-#define DVC_S2_SPX 2
-#endif
-constexpr int SPX = DVC_S2_SPX;         // solve pixels a thread: rows (SPX r .. SPX r + SPX-1) of a wave's 64 columns
+// Role map of the M waves (wv = 1..15), a nibble per wave (15 = none): the
+// wave's vertical-chain slot, solve slot and position slot. Waves w, w+4,
+// w+8, w+12 share a SIMD (a workgroup's waves go to the SIMDs cyclically):
+// V 1,2,3,5,6,7; S 9,10,11,13,14,15; the chain's mates 4, 8, 12 positions
+// only (the partial and the empty position slot on 8 and 12). Other maps —
+// solve waves on the chain's SIMD, one 3-row solve wave a SIMD, S and V
+// swapped — measured −1.7 … +0.6 % (experiments/README.md, round 5).
+constexpr unsigned long long S2_VTAB = 0xffffffff543f210full, S2_STAB = 0x543f210fffffffffull,
+                             S2_GTAB = 0xba9e876d543c210full;
+constexpr int SPX = 2;                  // solve pixels a thread: rows (SPX r .. SPX r + SPX-1) of a wave's 64 columns
 static_assert(NV <= 6 * 64 && RB * NC <= 15 * 64 && RB == 6 * SPX && NT == 16 * 64, "thread roles (k_flow_scan2)");
+__device__ __forceinline__ int s2_slot(unsigned long long tab, int wv)
+{
+    const int v = (int)((tab >> (4 * wv)) & 15ull);
+    return v == 15 ? -1 : v;
+}
 static_assert(RB * 5 <= 64, "a block's horizontal chains fit one wave");
 static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "16-B lines on distinct banks");
 }  // namespace scan2
@@ -1521,6 +1532,9 @@ __device__ unsigned long long g_scan2_stamps[32 * 96 * 8];
     g_scan2_stamps[(s * 96 + (kk) + 1) * 8 + (j)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP2(tt, kk, j) do {} while (0)
+#endif
+#ifndef DVC_STAMP_DETAIL
+#define DVC_STAMP_DETAIL 0   // 1: stamps 4..7 trace wave 10 (S + G) through its interval
 #endif
 // One role's item loop (CHAIN: wave 0; else the M waves): both take the same
 // items and run the same barriers; split at the top so that no value of one
@@ -1639,15 +1653,14 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
             // Roles by wave (wv = 1..15). Waves 0, 4, 8, 12 share a SIMD (a
             // workgroup's waves go to the SIMDs cyclically), so the chain wave's
             // SIMD mates 4, 8, 12 take the light role (positions only) and the
-            // position slots left over (RB x NC < 15 x 64) fall on wave 12:
+            // position slots left over (RB x NC < 15 x 64) fall on waves 8 and 12:
             //   vertical chains + positions:   waves 1, 2, 3, 5, 6, 7
             //   solve (SPX rows) + positions:  waves 9, 10, 11, 13, 14, 15
             //   positions only:                waves 4, 8, 12
             const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-            const bool light = (wv & 3) == 0;
-            const int vslot = wv <= 7 && !light ? wv - 1 - wv / 4 : -1;               // 0..5
-            const int sslot = wv >= 9 && !light ? wv - 9 - (wv >= 13 ? 1 : 0) : -1;   // 0..5
-            const int gslot = light ? 11 + wv / 4 : wv - 1 - wv / 4;                 // 0..14
+            const int vslot = s2_slot(S2_VTAB, wv);   // 0..5
+            const int sslot = s2_slot(S2_STAB, wv);   // 0 .. RB/SPX - 1
+            const int gslot = s2_slot(S2_GTAB, wv);   // 0..14
             // vertical chain of this thread (channel-major: consecutive threads,
             // consecutive columns of one channel)
             const int vidx = vslot * 64 + lane;
@@ -1715,6 +1728,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
             auto interval = [&](int k, MatPos<1>& X, MatPos<1>& Y) -> bool {
                 mat_stage3<1>(A, X, tb0, k + 2 < NB);   // G(k+2) -> transfer buffer (k+2) % 2 (always
                                                         // computed: the loads are consumed on every path)
+                if (DVC_STAMP_DETAIL && tid == 640) STAMP2(t, k, 4);   // (detail stamps: wave 10's steps)
                 // G(k+3): R loads this interval. Every load below is issued
                 // unconditionally (positions are clamped, so always valid; past the
                 // last block they are simply unused): a load under a branch makes
@@ -1768,8 +1782,10 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                     }
                 };
                 __builtin_amdgcn_sched_barrier(0);
+                if (DVC_STAMP_DETAIL && tid == 640) STAMP2(t, k, 5);
                 ldR1(Y, 0);
                 __builtin_amdgcn_sched_barrier(0);
+                if (DVC_STAMP_DETAIL && tid == 640) STAMP2(t, k, 6);
                 // V(k+1), rows 0..5 / R row 1 / rows 6..11
                 const int vb = k + 1;
                 const float* t0 = tb0 + (size_t)(vb & 1) * TB + vj * 5 + vc;
@@ -1782,10 +1798,10 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 flowld(X, k + 4);
                 __builtin_amdgcn_sched_barrier(0);
                 solve_store();
-                if (tid == 64) STAMP2(t, k, 4);      // arrival at the barrier: wave 1 (V + G)
-                if (tid == 256) STAMP2(t, k, 5);     // wave 4 (G, the chain's SIMD)
-                if (tid == 640) STAMP2(t, k, 6);     // wave 10 (S + G)
-                if (tid == 960) STAMP2(t, k, 7);     // wave 15 (S + G)
+                if (!DVC_STAMP_DETAIL && tid == 64) STAMP2(t, k, 4);    // arrival at the barrier: wave 1 (V + G)
+                if (!DVC_STAMP_DETAIL && tid == 256) STAMP2(t, k, 5);   // wave 4 (G, the chain's SIMD)
+                if (!DVC_STAMP_DETAIL && tid == 640) STAMP2(t, k, 6);   // wave 10 (S + G)
+                if (tid == (DVC_STAMP_DETAIL ? 640 : 960)) STAMP2(t, k, 7);   // wave 15 (S + G) / wave 10
                 __syncthreads();
                 return s_alive != 0;
             };

@@ -4,7 +4,8 @@ of the last level-0 launch, every (strip, interval). Chain wave: 0 start, 1
 after the left-strip poll, 2 after the chain, 3 after the barrier. An M-wave
 waves' arrivals at the interval's barrier: 4 wave 1 (vertical sums + M), 5
 wave 4 (M only, on the chain's SIMD), 6 wave 10 (solve + M), 7 wave 15
-(solve + M)."""
+(solve + M). With -DDVC_STAMP_DETAIL=1 (and DVC_STAMP_DETAIL=1 here) stamps
+4..7 trace wave 10 instead: after stage 3, after the solve, after R1 row 0, at the barrier."""
 import ctypes
 import os
 import sys
@@ -46,6 +47,14 @@ rows = {
     "wave 15 (S+G) done": st[:, :, 7] - prev3,
     "interval": st[:, :, 3] - prev3,
 }
+if os.environ.get("DVC_STAMP_DETAIL") == "1":   # library built with -DDVC_STAMP_DETAIL=1: wave 10's steps
+    rows = {k: v for k, v in rows.items() if k.startswith("chain") or k == "interval"}
+    rows.update({
+        "w10: to stage3 done": st[:, :, 4] - prev3,
+        "w10: ldR0 + solve": st[:, :, 5] - st[:, :, 4],
+        "w10: ldR1 row 0": st[:, :, 6] - st[:, :, 5],
+        "w10: rest to barrier": st[:, :, 7] - st[:, :, 6],
+    })
 for nm, d in rows.items():
     d = d / cyc
     print(f"{nm:22s} median {np.median(d):7.3f} us  p10 {np.percentile(d, 10):7.3f}  p90 {np.percentile(d, 90):7.3f}"
