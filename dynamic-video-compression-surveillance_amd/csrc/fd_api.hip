@@ -839,7 +839,8 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     const int obytes = (opitch % 4) || (ostride % 4) || ((uintptr_t)ov & 3) || ((uintptr_t)cp & 3);
     const bool out_i420 = h->p.flags & DVC_FLAG_OUT_I420;
     // fused front (fd_kernels.h FrontOut): block_size 4, BGR frames or 4:2:0
-    // surfaces read in place (or staged), BGR outputs in dword rows;
+    // surfaces read in place (or staged), BGR outputs in dword rows or I420
+    // frames (DVC_FLAG_OUT_I420: the front and k_fix4 write BGR2YUV_I420);
     // DVC_FD_FUSED=0 turns it off (A/B)
     static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
     // (B = 4: k_fix4 scans a block row's static words in one wave, SW <= 64;
@@ -847,8 +848,9 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     // per-block pass. Not the default: the 8x8 DCT at four lanes a block makes
     // the VALU-bound front the period — 268-270 k against 288 k Mpx/s for the
     // one-pass k_out<8> at the __main__ kwargs, experiments/README.md)
-    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && !out_i420 && !obytes && (ov || cp) &&
-                       ((h->B == 4 && h->SW <= 64) || (h->B == 8 && h->fused8 && sf.fmt == DVC_FMT_BGR));
+    const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && !obytes && (ov || cp) &&
+                       ((h->B == 4 && h->SW <= 64) ||
+                        (h->B == 8 && h->fused8 && sf.fmt == DVC_FMT_BGR && !out_i420));
     {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
         const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
         S.olo[0] = (uintptr_t)ov;
@@ -881,6 +883,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         fo.qinv = 1.0 / (double)h->p.quant;
         fo.M = h->M;
         fo.B = h->B;
+        fo.i420 = out_i420 ? 1 : 0;
     }
     // KTIMING: events around the dominant HBM kernel — the fused front on
     // s_front, else k_out on s_out

@@ -172,6 +172,7 @@ struct FrontOut {
     double qinv;
     DctMat M;          // B x B basis
     int B;             // block size: 4, or 8 (BGR frames in, NW = 4 tiles)
+    int i420;          // outputs as BGR2YUV_I420 frames (B = 4, NW = 4): Y plane W x H, U, V of W/2 x H/2
 };
 // frames t = 0..n-1 at bgr + t*fstride; gray_in = the previous blurred gray,
 // gray_out := frame n-1's (distinct buffers); motion mask of frame t -> mbits + t*H*WW;

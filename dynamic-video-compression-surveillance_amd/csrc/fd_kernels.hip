@@ -226,17 +226,96 @@ __device__ __forceinline__ void dct8_quad(float* S, int r, const float (&x)[2][8
     wave_sync_lds();   // the scratch is rewritten by the next frame
 }
 
+// One row of a BxB block of an output frame as the encoder's 4:2:0 input
+// (cvtColor BGR2YUV_I420, include/dvc.h DVC_FLAG_OUT_I420): B luma bytes, and
+// on even rows the B/2 chroma samples of the 2x2 quads (their top-left pixel).
+// I420 frame at f: Y plane W x H, then U and V planes of W/2 x H/2.
+template <int B>
+__device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, int x, const uint32_t* w)
+{
+    using namespace yuvpx;
+    uint32_t yv[B], uv[B / 2], vv[B / 2];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+        const int b = (int)((w[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255);
+        const int g = (int)((w[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255);
+        const int r = (int)((w[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255);
+        yv[j] = luma(b, g, r);
+        if (!(j & 1)) {
+            uv[j >> 1] = chroma_u(b, g, r);
+            vv[j >> 1] = chroma_v(b, g, r);
+        }
+    }
+    uint32_t* yo = reinterpret_cast<uint32_t*>(f + (size_t)y * W + x);
+#pragma unroll
+    for (int d = 0; d < B / 4; ++d)
+        __builtin_nontemporal_store(pack4(yv[4 * d], yv[4 * d + 1], yv[4 * d + 2], yv[4 * d + 3]), yo + d);
+    if (!(y & 1)) {
+        const size_t c = (size_t)W * H + (size_t)(y >> 1) * (W >> 1) + (x >> 1), q = (size_t)(W >> 1) * (H >> 1);
+        if constexpr (B == 4) {
+            __builtin_nontemporal_store((uint16_t)(uv[0] | (uv[1] << 8)), reinterpret_cast<uint16_t*>(f + c));
+            __builtin_nontemporal_store((uint16_t)(vv[0] | (vv[1] << 8)), reinterpret_cast<uint16_t*>(f + c + q));
+        } else {
+#pragma unroll
+            for (int d = 0; d < B / 8; ++d) {
+                __builtin_nontemporal_store(pack4(uv[4 * d], uv[4 * d + 1], uv[4 * d + 2], uv[4 * d + 3]),
+                                            reinterpret_cast<uint32_t*>(f + c) + d);
+                __builtin_nontemporal_store(pack4(vv[4 * d], vv[4 * d + 1], vv[4 * d + 2], vv[4 * d + 3]),
+                                            reinterpret_cast<uint32_t*>(f + c + q) + d);
+            }
+        }
+    }
+}
+
+
+// BGR2YUV_I420 luma of the 4 packed BGR pixels of a quad row (dwords d0..d2),
+// as v_dot4 with the 20-bit coefficients split into bytes: the same integer as
+// yuvpx::luma (no saturation needed: 16 <= Y <= 235 for every BGR).
+__device__ __forceinline__ uint32_t luma4_i420(uint32_t d0, uint32_t d1, uint32_t d2)
+{
+    using namespace yuvpx;
+    constexpr uint32_t K0 = (CBY & 255) | ((CGY & 255) << 8) | ((CRY & 255) << 16);
+    constexpr uint32_t K1 = ((CBY >> 8) & 255) | (((CGY >> 8) & 255) << 8) | (((CRY >> 8) & 255) << 16);
+    constexpr uint32_t K2 = (CBY >> 16) | ((CGY >> 16) << 8) | ((CRY >> 16) << 16);
+    static_assert((CBY >> 24) == 0 && (CGY >> 24) == 0 && (CRY >> 24) == 0 && CBY > 0 && CGY > 0 && CRY > 0,
+                  "luma coefficients: three bytes each");
+    static_assert((255 * (CBY + CGY + CRY) + HALF + (16 << SHIFT)) >> SHIFT <= 255, "luma never saturates");
+    const uint32_t p[4] = {d0, __builtin_amdgcn_alignbyte(d1, d0, 3), __builtin_amdgcn_alignbyte(d2, d1, 2), d2 >> 8};
+    uint32_t y[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t t2 = __builtin_amdgcn_udot4(p[j] & 0x00ffffffu, K2, 0u, false);
+        const uint32_t t1 = __builtin_amdgcn_udot4(p[j] & 0x00ffffffu, K1, t2 << 8, false);
+        y[j] = __builtin_amdgcn_udot4(p[j] & 0x00ffffffu, K0, (t1 << 8) + (uint32_t)(HALF + (16 << SHIFT)), false) >> SHIFT;
+    }
+    return yuvpx::pack4(y[0], y[1], y[2], y[3]);
+}
+// chroma of pixels 0 and 2 of the quad row (the top-left pixels of its two
+// 2x2 quads): U0 | U2 << 8 in the low half, V0 | V2 << 8 in the high half
+__device__ __forceinline__ uint32_t chroma2_i420(uint32_t d0, uint32_t d1, uint32_t d2)
+{
+    using namespace yuvpx;
+    const int b0 = d0 & 255, g0 = (d0 >> 8) & 255, r0 = (d0 >> 16) & 255;
+    const int b2 = (d1 >> 16) & 255, g2 = d1 >> 24, r2 = d2 & 255;   // bytes 6, 7, 8
+    return chroma_u(b0, g0, r0) | (chroma_u(b2, g2, r2) << 8) | (chroma_v(b0, g0, r0) << 16) |
+           (chroma_v(b2, g2, r2) << 24);
+}
+// a gray pixel (R = G = B = u) has U = V = 128: both chroma rows of coefficients sum to 1
+static_assert(yuvpx::CRU + yuvpx::CGU + yuvpx::CBU == 1 && yuvpx::CBU + yuvpx::CGV + yuvpx::CBV == 1,
+              "gray chroma is 128");
+
 #ifndef DVC_FRONT_WGS_B8   // fused 8x8 blocks: 3 workgroups a CU (4 spill 20 VGPRs)
 #define DVC_FRONT_WGS_B8 3
 #endif
-template <int NW, int PF, int FMT, bool OUT, int OB = 4>
-__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+template <int NW, int PF, int FMT, bool OUT, int OB = 4, bool OI = false>
+__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : OI ? 4 : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
 {
     static_assert(!OUT || NW == 4 || NW == 8, "fused outputs: 16- or 32-row tiles");
     static_assert(!OUT || OB == 4 || (OB == 8 && NW == 4), "fused 8x8 blocks: 16-row tiles (64 blocks, 4 lanes each)");
+    static_assert(!OI || (OUT && OB == 4 && NW == 4), "fused I420 outputs: 4x4 blocks, 16-row tiles");
     constexpr int FT_H = 4 * NW, FT_R = FT_H + 4, NT = 64 * NW;
     constexpr bool B8 = OUT && OB == 8;
     __shared__ uint32_t sg[FT_R][FT_Q];        // gray quads
@@ -374,10 +453,15 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
         o8[ii] = B8 ? (uint32_t)((size_t)(y0 + 8 * by8 + 2 * r8 + ii) * fo.opitch + 3 * (size_t)(x0 + 8 * bx8)) : 0u;
     // OUT rows and motion-bit words: per-lane 32-bit offsets from the frame's
     // wave-uniform base (through voff once per frame, like the loads)
-    uint32_t oro[4], mwo[4];
+    uint32_t oro[4], mwo[4], cro[2];   // OI: oro = luma rows, cro = the U rows of row pairs 0-1, 2-3
+    const uint32_t cq = OI ? (uint32_t)((W >> 1) * (H >> 1)) : 0u;   // U plane -> V plane
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        cro[k] = OI ? (uint32_t)((size_t)W * H + (size_t)((y0 + 4 * wave) / 2 + k) * (W >> 1) + (x >> 1)) : 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        oro[i] = OUT ? (uint32_t)((size_t)(y0 + 4 * wave + i) * fo.opitch + 3 * (size_t)x) : 0u;
+        oro[i] = OI  ? (uint32_t)((size_t)(y0 + 4 * wave + i) * W + x)
+                 : OUT ? (uint32_t)((size_t)(y0 + 4 * wave + i) * fo.opitch + 3 * (size_t)x) : 0u;
         mwo[i] = (uint32_t)(min(y0 + orow(i), H - 1) * WW + min((x0 >> 6) + (lane >> 4), WW - 1)) * 8u + ((lane >> 1) & 4u);
     }
     auto frame = [&](Quads& qs, int t) {
@@ -385,6 +469,10 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
         for (int i = 0; i < 4; ++i) {
             if constexpr (OUT) oro[i] = voff(oro[i]);
             mwo[i] = voff(mwo[i]);
+        }
+        if constexpr (OI) {
+            cro[0] = voff(cro[0]);
+            cro[1] = voff(cro[1]);
         }
         if constexpr (B8) {
             o8[0] = voff(o8[0]);
@@ -415,12 +503,26 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
             // registers are reloaded with frame t + PF right after the barrier
             if (fo.ov && full_blk && t >= t_first) {
                 uint8_t* o = fo.ov + (size_t)t * fo.ostride;
+                if constexpr (OI) {   // the frame as BGR2YUV_I420 (rows 4 wave + j: even rows carry the chroma)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[j]);
-                    __builtin_nontemporal_store(cb[j][0], r);
-                    __builtin_nontemporal_store(cb[j][1], r + 1);
-                    __builtin_nontemporal_store(cb[j][2], r + 2);
+                    for (int j = 0; j < 4; ++j) {
+                        __builtin_nontemporal_store(luma4_i420(cb[j][0], cb[j][1], cb[j][2]),
+                                                    reinterpret_cast<uint32_t*>(o + oro[j]));
+                        if (!(j & 1)) {
+                            const uint32_t uv = chroma2_i420(cb[j][0], cb[j][1], cb[j][2]);
+                            __builtin_nontemporal_store((uint16_t)uv, reinterpret_cast<uint16_t*>(o + cro[j >> 1]));
+                            __builtin_nontemporal_store((uint16_t)(uv >> 16),
+                                                        reinterpret_cast<uint16_t*>(o + (cro[j >> 1] + cq)));
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[j]);
+                        __builtin_nontemporal_store(cb[j][0], r);
+                        __builtin_nontemporal_store(cb[j][1], r + 1);
+                        __builtin_nontemporal_store(cb[j][2], r + 2);
+                    }
                 }
             }
         }
@@ -566,11 +668,24 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
 #pragma unroll
                     for (int j = 0; j < 4; ++j)   // clip to [0, 255], truncating uint8 cast
                         u[j] = (uint32_t)__builtin_amdgcn_fmed3f(X[4 * i + j] + 128.0f, 0.0f, 255.0f);
-                    gray_bgr4(u[0], u[1], u[2], u[3], cw);
-                    uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[i]);
-                    __builtin_nontemporal_store(cw[0], r);
-                    __builtin_nontemporal_store(cw[1], r + 1);
-                    __builtin_nontemporal_store(cw[2], r + 2);
+                    if constexpr (OI) {   // Y of (u, u, u); U = V = 128
+                        uint32_t yv[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) yv[j] = yuvpx::luma((int)u[j], (int)u[j], (int)u[j]);
+                        __builtin_nontemporal_store(yuvpx::pack4(yv[0], yv[1], yv[2], yv[3]),
+                                                    reinterpret_cast<uint32_t*>(o + oro[i]));
+                        if (!(i & 1)) {
+                            __builtin_nontemporal_store((uint16_t)0x8080u, reinterpret_cast<uint16_t*>(o + cro[i >> 1]));
+                            __builtin_nontemporal_store((uint16_t)0x8080u,
+                                                        reinterpret_cast<uint16_t*>(o + (cro[i >> 1] + cq)));
+                        }
+                    } else {
+                        gray_bgr4(u[0], u[1], u[2], u[3], cw);
+                        uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[i]);
+                        __builtin_nontemporal_store(cw[0], r);
+                        __builtin_nontemporal_store(cw[1], r + 1);
+                        __builtin_nontemporal_store(cw[2], r + 2);
+                    }
                 }
             }
         }
@@ -1301,47 +1416,6 @@ __device__ __forceinline__ void store_row(uint8_t* dst, const uint32_t* w, int b
     }
 }
 
-// One row of a BxB block of an output frame as the encoder's 4:2:0 input
-// (cvtColor BGR2YUV_I420, include/dvc.h DVC_FLAG_OUT_I420): B luma bytes, and
-// on even rows the B/2 chroma samples of the 2x2 quads (their top-left pixel).
-// I420 frame at f: Y plane W x H, then U and V planes of W/2 x H/2.
-template <int B>
-__device__ __forceinline__ void store_i420_row(uint8_t* f, int W, int H, int y, int x, const uint32_t* w)
-{
-    using namespace yuvpx;
-    uint32_t yv[B], uv[B / 2], vv[B / 2];
-#pragma unroll
-    for (int j = 0; j < B; ++j) {
-        const int b = (int)((w[(3 * j) >> 2] >> (8 * ((3 * j) & 3))) & 255);
-        const int g = (int)((w[(3 * j + 1) >> 2] >> (8 * ((3 * j + 1) & 3))) & 255);
-        const int r = (int)((w[(3 * j + 2) >> 2] >> (8 * ((3 * j + 2) & 3))) & 255);
-        yv[j] = luma(b, g, r);
-        if (!(j & 1)) {
-            uv[j >> 1] = chroma_u(b, g, r);
-            vv[j >> 1] = chroma_v(b, g, r);
-        }
-    }
-    uint32_t* yo = reinterpret_cast<uint32_t*>(f + (size_t)y * W + x);
-#pragma unroll
-    for (int d = 0; d < B / 4; ++d)
-        __builtin_nontemporal_store(pack4(yv[4 * d], yv[4 * d + 1], yv[4 * d + 2], yv[4 * d + 3]), yo + d);
-    if (!(y & 1)) {
-        const size_t c = (size_t)W * H + (size_t)(y >> 1) * (W >> 1) + (x >> 1), q = (size_t)(W >> 1) * (H >> 1);
-        if constexpr (B == 4) {
-            __builtin_nontemporal_store((uint16_t)(uv[0] | (uv[1] << 8)), reinterpret_cast<uint16_t*>(f + c));
-            __builtin_nontemporal_store((uint16_t)(vv[0] | (vv[1] << 8)), reinterpret_cast<uint16_t*>(f + c + q));
-        } else {
-#pragma unroll
-            for (int d = 0; d < B / 8; ++d) {
-                __builtin_nontemporal_store(pack4(uv[4 * d], uv[4 * d + 1], uv[4 * d + 2], uv[4 * d + 3]),
-                                            reinterpret_cast<uint32_t*>(f + c) + d);
-                __builtin_nontemporal_store(pack4(vv[4 * d], vv[4 * d + 1], vv[4 * d + 2], vv[4 * d + 3]),
-                                            reinterpret_cast<uint32_t*>(f + c + q) + d);
-            }
-        }
-    }
-}
-
 #ifndef DVC_OUT_NTLOAD
 #define DVC_OUT_NTLOAD 0
 #endif
@@ -1582,7 +1656,8 @@ __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, in
             uint32_t ow[3];
 #pragma unroll
             for (int d = 0; d < 3; ++d) ow[d] = ((red[d] ^ b.px[i][d]) & m[d]) ^ b.px[i][d];
-            store_row<3>(a.overlay + fo + (o + (uint32_t)(i * a.opitch)), ow, 0);
+            if (a.out_i420) store_i420_row<4>(a.overlay + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, ow);
+            else store_row<3>(a.overlay + fo + (o + (uint32_t)(i * a.opitch)), ow, 0);
         }
     }
     if (a.compressed) {   // not static: the YCrCb -> BGR round trip of every pixel
@@ -1605,7 +1680,8 @@ __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, in
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 cw[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-            store_row<3>(a.compressed + fo + (o + (uint32_t)(i * a.opitch)), cw, 0);
+            if (a.out_i420) store_i420_row<4>(a.compressed + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, cw);
+            else store_row<3>(a.compressed + fo + (o + (uint32_t)(i * a.opitch)), cw, 0);
         }
     }
 }
@@ -2015,6 +2091,27 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
                     return;
                 }
             }
+            if constexpr (NW == 4) {
+                if (fo->i420) {   // I420 outputs (launch_front: B = 4, NW = 4)
+                    if (sf.fmt == DVC_FMT_NV12)
+                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_NV12, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                                           fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
+                                           xcd, *fo);
+                    else if (sf.fmt == DVC_FMT_I420)
+                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_I420, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                                           fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
+                                           xcd, *fo);
+                    else if (pf == 2)
+                        hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                                           fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
+                                           xcd, *fo);
+                    else
+                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                                           fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
+                                           xcd, *fo);
+                    return;
+                }
+            }
             if (sf.fmt == DVC_FMT_NV12)
                 hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
@@ -2051,10 +2148,11 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const Src
     if (fo && !(fo->B == 4 ? dct4_is_const(fo->M) : fo->B == 8 && dct8_is_const(fo->M)))
         return hipErrorInvalidValue;   // the fused DCT's constant basis
     if (fo && fo->B == 8 && sf.fmt != DVC_FMT_BGR) return hipErrorInvalidValue;   // 8x8: BGR frames only
+    if (fo && fo->i420 && (fo->B != 4 || g.W % 4 || g.H % 4)) return hipErrorInvalidValue;   // I420: 4x4, whole blocks
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
     static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
     if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
-    else if (nw == 8 && !(fo && fo->B == 8)) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
+    else if (nw == 8 && !(fo && (fo->B == 8 || fo->i420))) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     return hipGetLastError();
 }
@@ -2224,7 +2322,7 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
         return hipGetLastError();
     }
     if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR out in dword rows)
-        if (B != 4 || a.out_i420 || a.obytes) return hipErrorInvalidValue;
+        if (B != 4 || a.obytes) return hipErrorInvalidValue;   // (I420 outputs: whole 4x4 blocks, create checked)
         static const int fwgs = [] {   // DVC_FIX_WGS: k_fix4 workgroups (default 6 per CU: all resident at 79 VGPRs)
             if (const char* e = getenv("DVC_FIX_WGS")) return std::max(1, atoi(e));
             int dev = 0, cus = 256;

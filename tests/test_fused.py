@@ -1,7 +1,7 @@
 """GPU parity of the fused front (fd_kernels.h FrontOut) against the one-pass
 output stage, through the C-ABI.
 
-With block_size 4 and BGR outputs (BGR or 4:2:0 input), k_front writes every full 4x4
+With block_size 4 and BGR or I420 outputs (BGR or 4:2:0 input), k_front writes every full 4x4
 block of both outputs as if it were static (overlay = the frame, compressed =
 (Y', Y', Y') of the quantised DCT, frame_differencing.py:110-130) while it has
 the frame in registers, and k_fix4 rewrites the blocks the accumulated mask
@@ -296,3 +296,73 @@ def test_fused_nv12_bench_scale(gpu_lib, oracle_lib):
         assert torch.equal(outs[True][0][t], outs[False][0][t]), f"overlay: fused != unfused at frame {t}"
         assert torch.equal(outs[True][1][t], outs[False][1][t]), f"compressed: fused != unfused at frame {t}"
     del outs, seq, ring
+
+
+@pytest.mark.parametrize("W,H,n,batch,seed,noisy,fmt", [
+    (1920, 1080, 61, 20, 21, False, "BGR"),
+    (640, 360, 41, 13, 22, True, "BGR"),
+    (1000, 200, 21, 20, 24, True, "BGR"),      # tiles past the right edge
+    (1280, 720, 25, 12, 25, True, "NV12"),     # 4:2:0 surfaces read in place
+    (648, 360, 21, 8, 26, False, "I420"),
+])
+def test_fused_i420_outputs_equal_unfused(gpu_lib, oracle_lib, W, H, n, batch, seed, noisy, fmt):
+    """DVC_FLAG_OUT_I420 on the fused front: k_front writes every 4x4 block of
+    both outputs as BGR2YUV_I420 of the static form (overlay = the frame,
+    compressed = (Y', Y', Y') -> U = V = 128) and k_fix4 rewrites the
+    non-static blocks as I420; every byte equals the one-pass k_out path."""
+    import torch
+    from dvc_amd.synthetic import clip
+    from tests.test_video_io_gpu import _nv12
+    dev = torch.device("cuda", 0)
+    frames = clip(W, H, n, seed=seed, noisy=noisy)
+    if fmt == "BGR":
+        src = frames
+    else:
+        i420 = np.stack([oracle_lib.bgr_to_i420(f) for f in frames])
+        src = i420 if fmt == "I420" else np.stack([_nv12(f, H, W) for f in i420])
+    seq = torch.from_numpy(np.ascontiguousarray(src)).to(dev)
+    outs = {}
+    for fused in (True, False):
+        w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=batch, fused=fused, ktiming=True, in_format=fmt,
+                             out_format="I420")
+        w.prime(seq[0])
+        ov = torch.empty((n - 1, H * 3 // 2, W), dtype=torch.uint8, device=dev)
+        cp = torch.empty_like(ov)
+        for b0 in range(1, n, batch):
+            b1 = min(n, b0 + batch)
+            w.step_batch(seq[b0:b1], ov[b0 - 1:b1 - 1], cp[b0 - 1:b1 - 1])
+        w.sync()
+        assert w.ktime_kernel() == ("k_front_fused" if fused else "k_out")
+        outs[fused] = (ov, cp, w.stats())
+        w.close()
+    (ovf, cpf, sf), (ovu, cpu_, su) = outs[True], outs[False]
+    assert sf == su
+    for t in range(n - 1):
+        assert torch.equal(ovf[t], ovu[t]), f"overlay (I420): fused != unfused at frame {t + 1}"
+        assert torch.equal(cpf[t], cpu_[t]), f"compressed (I420): fused != unfused at frame {t + 1}"
+
+
+def test_fused_i420_outputs_match_oracle(gpu_lib, oracle_lib):
+    """The fused I420 outputs at the bench's launch size against the oracle's
+    BGR outputs converted by the oracle's BGR2YUV_I420 (fd:112,131)."""
+    import torch
+    from dvc_amd.synthetic import clip
+    W, H, n = 1920, 1080, 9
+    frames = clip(W, H, n, seed=27, noisy=True)
+    dev = torch.device("cuda", 0)
+    seq = torch.from_numpy(frames).to(dev)
+    w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=n - 1, out_format="I420", ktiming=True)
+    w.prime(seq[0])
+    ov = torch.empty((n - 1, H * 3 // 2, W), dtype=torch.uint8, device=dev)
+    cp = torch.empty_like(ov)
+    w.step_batch(seq[1:], ov, cp)
+    w.sync()
+    assert w.ktime_kernel() == "k_front_fused"
+    w.close()
+    ref = oracle_lib.OracleFD(W, H)
+    ref.prime(frames[0])
+    for t in range(1, n):
+        rov, rcp, _ = ref.step(frames[t])
+        assert np.array_equal(ov[t - 1].cpu().numpy(), oracle_lib.bgr_to_i420(rov)), f"overlay (I420) at {t}"
+        assert np.array_equal(cp[t - 1].cpu().numpy(), oracle_lib.bgr_to_i420(rcp)), f"compressed (I420) at {t}"
+    ref.close()
