@@ -304,11 +304,14 @@ __device__ __forceinline__ uint32_t chroma2_i420(uint32_t d0, uint32_t d1, uint3
 static_assert(yuvpx::CRU + yuvpx::CGU + yuvpx::CBU == 1 && yuvpx::CBU + yuvpx::CGV + yuvpx::CBV == 1,
               "gray chroma is 128");
 
+#ifndef DVC_FRONT_WGS_YUV_OI   // 4:2:0 input, I420 outputs
+#define DVC_FRONT_WGS_YUV_OI 4
+#endif
 #ifndef DVC_FRONT_WGS_B8   // fused 8x8 blocks: 3 workgroups a CU (4 spill 20 VGPRs)
 #define DVC_FRONT_WGS_B8 3
 #endif
 template <int NW, int PF, int FMT, bool OUT, int OB = 4, bool OI = false>
-__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : OI ? 4 : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : OI ? DVC_FRONT_WGS_YUV_OI : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)
@@ -492,20 +495,9 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
                     cb[j][2] = qs.v2[j];
                 }
                 sg[lrow(j)][lane + 1] = gray4_dot(cb[j][0], cb[j][1], cb[j][2]);
-            }
-        }
-#pragma unroll
-        for (int j = OUT ? 4 : 0; j < NR; ++j)
-            if (NR * NW == FT_R || lrow(j) < FT_R)
-                sg[lrow(j)][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
-        if constexpr (OUT) {
-            // overlay := the frame (a static block has no acc > 127 pixel); the
-            // registers are reloaded with frame t + PF right after the barrier
-            if (fo.ov && full_blk && t >= t_first) {
-                uint8_t* o = fo.ov + (size_t)t * fo.ostride;
-                if constexpr (OI) {   // the frame as BGR2YUV_I420 (rows 4 wave + j: even rows carry the chroma)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                if constexpr (OI) {   // the frame as BGR2YUV_I420, row by row (rows 4 wave + j: even rows carry the chroma)
+                    if (fo.ov && full_blk && t >= t_first) {
+                        uint8_t* o = fo.ov + (size_t)t * fo.ostride;
                         __builtin_nontemporal_store(luma4_i420(cb[j][0], cb[j][1], cb[j][2]),
                                                     reinterpret_cast<uint32_t*>(o + oro[j]));
                         if (!(j & 1)) {
@@ -515,14 +507,24 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
                                                         reinterpret_cast<uint16_t*>(o + (cro[j >> 1] + cq)));
                         }
                     }
-                } else {
+                }
+            }
+        }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[j]);
-                        __builtin_nontemporal_store(cb[j][0], r);
-                        __builtin_nontemporal_store(cb[j][1], r + 1);
-                        __builtin_nontemporal_store(cb[j][2], r + 2);
-                    }
+        for (int j = OUT ? 4 : 0; j < NR; ++j)
+            if (NR * NW == FT_R || lrow(j) < FT_R)
+                sg[lrow(j)][lane + 1] = quad_gray<FMT>(qs.v0[j], qs.v1[j], qs.v2[j]);
+        if constexpr (OUT) {
+            // overlay := the frame (a static block has no acc > 127 pixel); the
+            // registers are reloaded with frame t + PF right after the barrier
+            if (!OI && fo.ov && full_blk && t >= t_first) {   // (OI: written row by row above)
+                uint8_t* o = fo.ov + (size_t)t * fo.ostride;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t* r = reinterpret_cast<uint32_t*>(o + oro[j]);
+                    __builtin_nontemporal_store(cb[j][0], r);
+                    __builtin_nontemporal_store(cb[j][1], r + 1);
+                    __builtin_nontemporal_store(cb[j][2], r + 2);
                 }
             }
         }
