@@ -912,11 +912,13 @@ __global__ void __launch_bounds__(256) k_merge(CclBufs cb, RowGeom g, int BH)
 }
 
 // The per-row kernels below (paint, resolve, area) give each row a group of
-// CG = 16 lanes — 4 rows per wave, 16 per workgroup — so one wave carries four
-// independent global-memory dependency chains (the union-find walks); a row's
-// runs are strided over its 16 lanes. LDS: one mask row per group.
-constexpr int CG = 16, CG_ROWS = 4 * (64 / CG);
+// CG lanes — CG = 16: 4 rows per wave, 16 per workgroup; CG = 8 (batches of
+// >= 64 frames, launch_ccl): 8 rows per wave, 32 per workgroup — so one wave
+// carries several independent global-memory dependency chains (the union-find
+// walks); a row's runs are strided over its CG lanes. LDS: one mask row per group.
+template <int CG> constexpr int cg_rows() { return 4 * (64 / CG); }
 
+template <int CG>
 __device__ __forceinline__ int group_incl_scan(int v)
 {
     const int sl = threadIdx.x & (CG - 1);
@@ -931,6 +933,7 @@ __device__ __forceinline__ int group_incl_scan(int v)
 // ------------------------------------------------------------------ paint ---
 // The kept (filtered) mask, fd:101-104 — every run of a kept component plus
 // the holes between its runs (drawContours FILLED).
+template <int CG>
 __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t min_area2)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -943,7 +946,7 @@ __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t mi
     uint64_t* __restrict__ kbits = fb.kbits;
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_k[];
     const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1);
-    const int y = blockIdx.x * CG_ROWS + slot;
+    const int y = blockIdx.x * cg_rows<CG>() + slot;
     const bool act = y < g.H;
     unsigned long long* s_k = lds_k + (size_t)slot * g.WW;
     if (act)
@@ -978,6 +981,7 @@ __global__ void __launch_bounds__(256) k_paint(CclBufs cb, RowGeom g, int64_t mi
 // Gaps whose root is OUTSIDE are E; the rest are holes: painted into the
 // filled row F = not E, and the runs either side of a hole united (the
 // component inside a hole of another joins the external one enclosing it).
+template <int CG>
 __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -991,7 +995,7 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
     uint64_t* __restrict__ fbits = fb.fbits;
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_r[];
     const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1);
-    const int y = blockIdx.x * CG_ROWS + slot;
+    const int y = blockIdx.x * cg_rows<CG>() + slot;
     const bool act = y < g.H;
     unsigned long long* s_f = lds_r + (size_t)slot * g.WW;
     // a row without runs is one gap touching both image borders: outside (E),
@@ -1029,6 +1033,7 @@ __global__ void __launch_bounds__(256) k_resolve(CclBufs cb, RowGeom g)
 // Row y with F row y+1 staged in LDS. 2*area per filled run:
 //   2*popc(F'[s..e]) - F'(s) - F'(e) + [F'(s-1)&F'(s)] + [F'(e)&F'(e+1)]
 // (F' = row y+1), split additively over the runs and holes of the filled run.
+template <int CG>
 __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
 {
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -1043,7 +1048,7 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
     extern __shared__ __attribute__((aligned(16))) unsigned long long lds_b[];
     const int lane = threadIdx.x & 63;
     const int slot = threadIdx.x / CG, sl = threadIdx.x & (CG - 1), g0 = lane & ~(CG - 1);
-    const int y = blockIdx.x * CG_ROWS + slot;
+    const int y = blockIdx.x * cg_rows<CG>() + slot;
     const bool act = y < g.H;
     unsigned long long* s_b = lds_b + (size_t)slot * g.WW;
     const bool last = y == g.H - 1;
@@ -1058,7 +1063,7 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
         const uint32_t base = fb.rowb[2 * y];
         const uint8_t* ge = gE + (fb.rowb[2 * y + 1] - 1);
         const uint64_t* b = reinterpret_cast<const uint64_t*>(s_b);
-        const unsigned long long gmask = 0xffffull << g0;
+        const unsigned long long gmask = ((1ull << CG) - 1ull) << g0;
         for (int k0 = 0; k0 < n; k0 += CG) {   // uniform trip count within the group: it reduces below
             const int k = k0 + sl;
             const bool valid = k < n;
@@ -1092,7 +1097,7 @@ __global__ void __launch_bounds__(256) k_area(CclBufs cb, RowGeom g)
             const unsigned long long heads = __ballot(head) & gmask;
             const unsigned long long after = heads & (lane == 63 ? 0ull : (~0ull << (lane + 1)));
             const int seg_end = after ? __builtin_ctzll(after) - 1 : g0 + CG - 1;
-            const int incl = group_incl_scan(c);
+            const int incl = group_incl_scan<CG>(c);
             const int seg = __shfl(incl, seg_end, 64) - incl + c;
             if (head && valid && seg) atomicAdd(area2 + r, (uint32_t)seg);
         }
@@ -2215,7 +2220,7 @@ int band_rows(const RowGeom&) { return BAND_ROWS; }
 size_t ccl_max_lds(const RowGeom& g)
 {
     return std::max({band_lds(g, BAND_ROWS, 1024), (size_t)8 * merge_lds_words(g.WW) * (256 / MG),
-                     (size_t)8 * g.WW * CG_ROWS});
+                     (size_t)8 * g.WW * cg_rows<8>()});
 }
 
 // Node budget of a band: 1024 (4 KB of parents beside the run index, ~14 KB
@@ -2251,11 +2256,24 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
                            8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
-    const int grows = (g.H + CG_ROWS - 1) / CG_ROWS;
-    const size_t glds = (size_t)8 * g.WW * CG_ROWS;
-    hipLaunchKernelGGL(k_resolve, dim3(grows, n), dim3(256), glds, s, c, g);
-    hipLaunchKernelGGL(k_area, dim3(grows, n), dim3(256), glds, s, c, g);
-    hipLaunchKernelGGL(k_paint, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
+    // row groups of 8 lanes (8 rows a wave) for batches of >= 128 frames, 16 below
+    // (1080p x 383: +0.8 to +2.0 %, noisy +2.6 %, x 128 +0.7 %; x 64 -1 %, x 32
+    // -4 %: the halved workgroup count no longer fills the device); DVC_CCL_CG overrides
+    static const int cg_env = [] { const char* e = getenv("DVC_CCL_CG"); return e ? atoi(e) : 0; }();
+    const int cg = cg_env == 8 || cg_env == 16 ? cg_env : (n >= 128 ? 8 : 16);
+    if (cg == 8) {
+        const int grows = (g.H + cg_rows<8>() - 1) / cg_rows<8>();
+        const size_t glds = (size_t)8 * g.WW * cg_rows<8>();
+        hipLaunchKernelGGL(k_resolve<8>, dim3(grows, n), dim3(256), glds, s, c, g);
+        hipLaunchKernelGGL(k_area<8>, dim3(grows, n), dim3(256), glds, s, c, g);
+        hipLaunchKernelGGL(k_paint<8>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
+    } else {
+        const int grows = (g.H + cg_rows<16>() - 1) / cg_rows<16>();
+        const size_t glds = (size_t)8 * g.WW * cg_rows<16>();
+        hipLaunchKernelGGL(k_resolve<16>, dim3(grows, n), dim3(256), glds, s, c, g);
+        hipLaunchKernelGGL(k_area<16>, dim3(grows, n), dim3(256), glds, s, c, g);
+        hipLaunchKernelGGL(k_paint<16>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
+    }
     return hipGetLastError();
 }
 
