@@ -727,9 +727,12 @@ __global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : P
 // unions run on the global parent arrays instead (monotone atomicMin links).
 // Small workgroups (4 waves, ~14 KB LDS at 1080p) keep the band stage schedulable
 // beside the streaming kernels of the other two streams. Dynamic LDS: band_lds().
-constexpr int BG = 16, BAND_ROWS = 256 / BG;
+#ifndef DVC_BAND_BG
+#define DVC_BAND_BG 16
+#endif
+constexpr int BG = DVC_BAND_BG, BAND_ROWS = 16, BAND_NT = BG * BAND_ROWS;
 
-__global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
+__global__ void __launch_bounds__(BAND_NT) k_band(CclBufs cb, RowGeom g, int budget)
 {
     constexpr int BH = BAND_ROWS;
     const CclBufs fb = cb.frame(blockIdx.y, g);
@@ -871,7 +874,10 @@ __global__ void __launch_bounds__(256) k_band(CclBufs cb, RowGeom g, int budget)
 // One group of MG lanes per band seam (rows b*BH-1 and b*BH): run indexes of
 // both rows in LDS, then global unions of the band roots with monotone
 // atomicMin links. 64/MG seams per wave, each its own dependency chain.
-constexpr int MG = 64;   // only ~H/8 seams per frame: a whole wave each keeps enough waves in flight
+#ifndef DVC_MERGE_MG
+#define DVC_MERGE_MG 64
+#endif
+constexpr int MG = DVC_MERGE_MG;   // only ~H/16 seams per frame: a whole wave each keeps enough waves in flight
 
 __host__ __device__ constexpr size_t merge_lds_words(int WW) { return (size_t)4 * WW + (size_t)(WW + 1); }
 
@@ -2252,7 +2258,7 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
         return hipSuccess;
     }
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
-    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(256), band_lds(g, BH, budget), s, c, g, budget);
+    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(BAND_NT), band_lds(g, BH, budget), s, c, g, budget);
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
                            8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
