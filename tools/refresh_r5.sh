@@ -30,6 +30,7 @@ b fd_per_frame --per-frame --runs 3 --steps 5 --warmup 1
 b fd_out_ring1 --out-ring 1 --runs 3
 b fd_b8_k10_r0.3 --block-size 8 --kernel-size 10 --release-factor 0.3 --runs 3
 b fd_i420_output --out-format I420 --runs 3
+b fd_nv12_input_i420_output --in-format NV12 --out-format I420 --runs 3
 bash tools/of_pmc.sh > $O/of_pmc.log 2>&1
 python3 tools/pmc_table.py $(find gpurun_out/of_pmc/p1 -name "p_counter_collection.csv" | head -1) \
     $(find gpurun_out/of_pmc/p2 -name "p_counter_collection.csv" | head -1) > $O/of_sq_counters.txt 2>&1 || true
