@@ -17,7 +17,7 @@ the 256 MB Infinity Cache); overlay and compressed outputs go to device buffers
 of the same length. A step = one pass over that sequence through
 dvc_fd_step_batch (launches of --batch frames, FD default 383 at 1080p: larger
 grids keep the latency-bound contour filter occupied and amortise each call's
-fixed serial tail — round 5 on one box: 32 → 296 k, 128 → 349 k, 383 → 368 k
+fixed serial tail — round 5 on one box: 32 → 311 k, 128 → 384 k, 383 → 394 k
 Mpx/s, profiles/r5_bench_fd_batch*.json; --per-frame: one dvc_fd_step per
 frame instead, 24 k).
 
@@ -32,7 +32,7 @@ world size the process group saw and every rank's own frame count.
 Extra JSON fields: ``roofline`` for the dominant kernel (FD: the fused k_front:
 hipEvent time per launch on the front stream where it runs, in a second pass of
 the same steps; k_out on the back stream when the one-pass output stage runs —
-block sizes other than 4, I420 outputs; ``copy``: the same bytes against this
+block sizes other than 4; ``copy``: the same bytes against this
 box's hand-written copy rate, dvc_copy_rate) and
 ``cpu_baseline`` (the C oracle, one host core, a bounded sample of the same
 feed, with ``all_cores``: one feed per available core up to the box's CPU
