@@ -1461,7 +1461,7 @@ static_assert((2 * P) % 64 != 0 && ((2 * P) / 4) % 2 == 1 && (2 * P) % 4 == 0, "
 // the 9 values a vertical chain subtracts next: a vector value (constant
 // element indices only), so it stays in registers (a float[9] passed by
 // reference went to scratch memory)
-typedef float Hist9 __attribute__((ext_vector_type(16)));
+typedef float Hist9 __attribute__((ext_vector_type(9)));
 
 // row I of a block at ring phase PH (y0 % 9 == PH), then the rows after it up
 // to I1: rows are loaded in groups of 3 (the group's LDS reads issued together)
