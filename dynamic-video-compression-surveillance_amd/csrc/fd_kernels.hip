@@ -2262,11 +2262,12 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
     if (nb > 1)
         hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
                            8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
-    // row groups of 8 lanes (8 rows a wave) for batches of >= 128 frames, 16 below
-    // (1080p x 383: +0.8 to +2.0 %, noisy +2.6 %, x 128 +0.7 %; x 64 -1 %, x 32
+    // row groups of 8 lanes (8 rows a wave) for launches of >= ~100 k rows (96
+    // frames at 1080p), 16 below (1080p x 383: +0.8 to +2.0 %, noisy +2.6 %,
+    // x 128 +0.7 %, x 96 +0.7 %, 4K x 95 +0.1 to +0.4 %; 1080p x 64 -1 %, x 32
     // -4 %: the halved workgroup count no longer fills the device); DVC_CCL_CG overrides
     static const int cg_env = [] { const char* e = getenv("DVC_CCL_CG"); return e ? atoi(e) : 0; }();
-    const int cg = cg_env == 8 || cg_env == 16 ? cg_env : (n >= 128 ? 8 : 16);
+    const int cg = cg_env == 8 || cg_env == 16 ? cg_env : ((long long)n * g.H >= 96LL * 1080 ? 8 : 16);
     if (cg == 8) {
         const int grows = (g.H + cg_rows<8>() - 1) / cg_rows<8>();
         const size_t glds = (size_t)8 * g.WW * cg_rows<8>();
