@@ -392,7 +392,7 @@ def main():
     ksteps = max(1, min(args.steps, 10), int(args.ktime_seconds / max(step_s, 1e-6)))
     run_steps([wk], ksteps)
     kms, kn = wk.ktime()
-    kkernel = "k_flow" if of else wk.ktime_kernel()
+    kkernel = wk.ktime_kernel()   # the library reports the kernel it launched (FD: front / k_out; OF: level 0)
     wk.close()
     kframes = ksteps * P
 
@@ -433,10 +433,7 @@ def main():
         if not of and (args.block_size, args.kernel_size, args.release_factor) != (4, 7, 0.5):
             workload += f"_b{args.block_size}_k{args.kernel_size}_r{args.release_factor:g}"
         if of:   # kn counts level-0 flow launches (iterations per batch)
-            # the library's level-0 kernel: the pipelined scan unless DVC_OF_SCAN2=0
-            # (the barrier-phased one) or --of-direct (direct per-pixel sums)
-            kname = ("k_flow" if args.of_direct else
-                     "k_flow_scan" if os.environ.get("DVC_OF_SCAN2") == "0" else "k_flow_scan2")
+            kname = kkernel   # the level-0 kernel the library launched (dvc_of_ktime_kernel)
             per_launch_frames = kframes * 2 / max(kn, 1)
             bytes_per_launch = OF_FLOW_BYTES_PER_PX * W * H * per_launch_frames
             traffic = pmc_traffic(os.path.join(ROOT, "profiles", "pmc_summary_of.json"), kname, workload,

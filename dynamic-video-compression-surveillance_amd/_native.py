@@ -31,6 +31,7 @@ DVC_FLAG_OF_DIRECT_SUMS = 0x10
 DVC_FLAG_OUT_I420 = 0x20
 DVC_FLAG_FD_UNFUSED = 0x40
 KTIME_OUT, KTIME_FRONT_FUSED = 0, 1         # dvc_fd_ktime_kernel: which kernel KTIMING timed
+KTIME_FLOW, KTIME_FLOW_SCAN, KTIME_FLOW_SCAN2 = 2, 3, 4   # dvc_of_ktime_kernel: the level-0 flow kernel
 FMT_BGR, FMT_I420, FMT_NV12 = 0, 1, 2      # DVC_FMT_* frame formats (video I/O)
 FORMATS = {"BGR": FMT_BGR, "I420": FMT_I420, "NV12": FMT_NV12}
 
@@ -46,7 +47,7 @@ EXPORTS = [
     "dvc_of_read_plane", "dvc_of_read_flow", "dvc_of_ktime", "dvc_of_destroy", "dvc_of_compress",
     "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free", "dvc_yuv420_to_bgr", "dvc_bgr_to_i420",
     "dvc_copy_rate", "dvc_ofc_create", "dvc_ofc_run", "dvc_ofc_sync", "dvc_ofc_destroy",
-    "dvc_fd_set_state", "dvc_of_set_state", "dvc_fd_ktime_kernel",
+    "dvc_fd_set_state", "dvc_of_set_state", "dvc_fd_ktime_kernel", "dvc_of_ktime_kernel",
 ]
 ABI_VERSION = 7
 MAX_BATCH = 512
@@ -177,6 +178,9 @@ def lib() -> ctypes.CDLL:
     if hasattr(L, "dvc_fd_ktime_kernel"):   # (an older build under DVC_LIB_PATH lacks it)
         L.dvc_fd_ktime_kernel.argtypes = [vp]
         L.dvc_fd_ktime_kernel.restype = ctypes.c_int
+    if hasattr(L, "dvc_of_ktime_kernel"):
+        L.dvc_of_ktime_kernel.argtypes = [vp]
+        L.dvc_of_ktime_kernel.restype = ctypes.c_int
     L.dvc_fd_destroy.argtypes = [vp]
     L.dvc_fd_destroy.restype = None
     L.dvc_gaussian_taps_q8.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_uint16)]

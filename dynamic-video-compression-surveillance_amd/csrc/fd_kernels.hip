@@ -1651,6 +1651,10 @@ __device__ __forceinline__ void fix4_load(const BackArgs& a, int t, int row, int
                      : (uint16_t)0;
 }
 
+// OI: I420 outputs (DVC_FLAG_OUT_I420) as a template parameter, so the BGR
+// fix-up carries no inlined I420 row store (63 -> 52 VGPRs, 32 -> 2 SGPR
+// spills for k_fix4<BGR>)
+template <bool OI>
 __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, int bx, const Fix4& b)
 {
     const size_t fo = (size_t)t * a.ostride;                            // wave-uniform
@@ -1669,7 +1673,7 @@ __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, in
             uint32_t ow[3];
 #pragma unroll
             for (int d = 0; d < 3; ++d) ow[d] = ((red[d] ^ b.px[i][d]) & m[d]) ^ b.px[i][d];
-            if (a.out_i420) store_i420_row<4>(a.overlay + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, ow);
+            if constexpr (OI) store_i420_row<4>(a.overlay + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, ow);
             else store_row<3>(a.overlay + fo + (o + (uint32_t)(i * a.opitch)), ow, 0);
         }
     }
@@ -1693,7 +1697,7 @@ __device__ __forceinline__ void fix4_store(const BackArgs& a, int t, int row, in
 #pragma unroll
             for (int d = 0; d < 3; ++d)
                 cw[d] = ob[4 * d] | (ob[4 * d + 1] << 8) | (ob[4 * d + 2] << 16) | ((uint32_t)ob[4 * d + 3] << 24);
-            if (a.out_i420) store_i420_row<4>(a.compressed + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, cw);
+            if constexpr (OI) store_i420_row<4>(a.compressed + fo, a.g.W, a.g.H, 4 * row + i, 4 * bx, cw);
             else store_row<3>(a.compressed + fo + (o + (uint32_t)(i * a.opitch)), cw, 0);
         }
     }
@@ -1714,7 +1718,7 @@ __device__ __forceinline__ int select_bit(uint64_t m, int r)
     return base + __builtin_ctz(v);
 }
 
-template <int FMT>
+template <int FMT, bool OI>
 __global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
 {
     const int lane = threadIdx.x & 63;
@@ -1754,7 +1758,7 @@ __global__ void __launch_bounds__(256) k_fix4(BackArgs a, int RG)
             const int row = row0 + s / SW, bx = (s % SW) * 64 + bit;
             Fix4 b;
             fix4_load<FMT>(a, t, row, bx, act, b);
-            if (act) fix4_store(a, t, row, bx, b);
+            if (act) fix4_store<OI>(a, t, row, bx, b);
         }
     }
 }
@@ -2361,9 +2365,13 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
         if (a.SW > 64) return hipErrorInvalidValue;   // rows of <= 64 words (W <= 16384 px): the scan's lanes
         const int RG = std::max(1, 64 / a.SW), units = (a.NBY + RG - 1) / RG * a.n;
         const dim3 fg(std::max(1, std::min(fwgs, (units + 3) / 4)));
-        if (a.sf.fmt == DVC_FMT_NV12) hipLaunchKernelGGL(k_fix4<DVC_FMT_NV12>, fg, dim3(256), 0, s, a, RG);
-        else if (a.sf.fmt == DVC_FMT_I420) hipLaunchKernelGGL(k_fix4<DVC_FMT_I420>, fg, dim3(256), 0, s, a, RG);
-        else hipLaunchKernelGGL(k_fix4<DVC_FMT_BGR>, fg, dim3(256), 0, s, a, RG);
+        const bool oi = a.out_i420;
+        if (a.sf.fmt == DVC_FMT_NV12 && oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_NV12, true>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_NV12) hipLaunchKernelGGL((k_fix4<DVC_FMT_NV12, false>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_I420 && oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_I420, true>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_I420) hipLaunchKernelGGL((k_fix4<DVC_FMT_I420, false>), fg, dim3(256), 0, s, a, RG);
+        else if (oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_BGR, true>), fg, dim3(256), 0, s, a, RG);
+        else hipLaunchKernelGGL((k_fix4<DVC_FMT_BGR, false>), fg, dim3(256), 0, s, a, RG);
     }
     else if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);

@@ -176,6 +176,12 @@ struct dvc_of {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     unsigned int epoch = 0;   // k_flow_scan launches so far (hand-off flags carry it)
+    int l0_kernel = -1;       // the level-0 flow kernel of the last batch (DVC_KTIME_FLOW*)
+    // DVC_OF_FAULT=scan_abort at create (fault injection, tests/test_of_gpu.py):
+    // every batch starts with the scan hand-off's abort flag raised, so each
+    // strip that polls fails at once and the launch drains; the next sync
+    // reports the error (the path a hand-off timeout takes)
+    bool fault_abort = false;
 };
 
 static void of_free(dvc_of* h)
@@ -399,7 +405,14 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     g.box_scale = 1. / (p.winsize * p.winsize);
     g.up = (float)(1. / p.pyr_scale);
     g.flow_thr = p.flow_threshold;
-    g.sliding = !(p.flags & DVC_FLAG_OF_DIRECT_SUMS);
+    // box sums: 0 direct per pixel (k_flow), 1 OpenCV's running order by the
+    // barrier-phased scan, 2 by the pipelined scan where it applies (winsize 9;
+    // of_launch_flow). DVC_OF_SCAN2=0 at create selects 1 (read per handle:
+    // tests compare the two scans, tests/test_of_gpu.py)
+    {
+        const char* e = getenv("DVC_OF_SCAN2");
+        g.sliding = (p.flags & DVC_FLAG_OF_DIRECT_SUMS) ? 0 : (e && atoi(e) == 0 ? 1 : 2);
+    }
     poly_coef(p.poly_n, p.poly_sigma, g.pc);   // FarnebackPolyExp(I, R, polyN, ...): n = poly_n
     dvc_host::dct_matrix(8, h->M);
     ellipse_rows(p.morph_kernel, g);           // of:62
@@ -567,6 +580,10 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
         if ((e = hipMemset(b.scan_g, 0, 16 * slots * mb)) != hipSuccess) return bad(e, "hipMemset");
     }
     if ((e = hipMemset(b.scan_abort, 0, 4)) != hipSuccess) return bad(e, "hipMemset");
+    {
+        const char* fe = getenv("DVC_OF_FAULT");
+        h->fault_abort = fe && std::strcmp(fe, "scan_abort") == 0;
+    }
     uint16_t vt[256];
     std::memset(vt, 0, sizeof(vt));
     for (int l = 1; l <= p.window; ++l) vt[l] = (uint16_t)vote_threshold(p.alpha_fraction, l);   // <= l + 1 <= 256
@@ -761,11 +778,13 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
             h->ev.push_back(e);
         }
     }
+    if (h->fault_abort) HIP_OK(hipMemsetAsync(h->b.scan_abort, 0xff, 4, h->s_flow));
     if (!(skip & 2)) HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, h->g.L, 1, h->s_flow, &h->epoch));
     HIP_OK(hipEventRecord(S.ev_l1, h->s_flow));
     if (timed) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_flow));
     if (!(skip & 2))
-        HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch, serial == 4 ? S.ev_l0a : nullptr));
+        HIP_OK(dvc::of_launch_flow(h->g, h->lv, h->b, a0, n, 0, 0, h->s_flow, &h->epoch, serial == 4 ? S.ev_l0a : nullptr,
+                                   &h->l0_kernel));
     if (timed) {
         HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_flow));
         h->ev_used += 2;
@@ -927,6 +946,13 @@ int dvc_of_ktime(dvc_of* h, double* total_ms, uint64_t* launches, int reset)
     if (launches) *launches = (h->ev_used / 2) * (uint64_t)h->g.iters;
     if (reset) h->ev_used = 0;
     return DVC_OK;
+}
+
+int dvc_of_ktime_kernel(const dvc_of* h)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    if (h->l0_kernel < 0) return fail(DVC_E_STATE, "no batch stepped yet");
+    return h->l0_kernel;
 }
 
 int dvc_of_debug_read(dvc_of* h, int what, int level, void* dst, int* w, int* hgt)

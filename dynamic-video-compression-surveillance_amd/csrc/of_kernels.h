@@ -71,7 +71,8 @@ struct OfGeom {
     double box_scale;  // 1 / (winsize * winsize)
     float up;          // (float)(1 / pyr_scale)
     float flow_thr;
-    int sliding;       // box sums in OpenCV's running order (k_flow_scan) / direct per pixel (k_flow)
+    int sliding;       // box sums: 0 direct per pixel (k_flow); OpenCV's running order by 1 k_flow_scan,
+                       // 2 k_flow_scan2 where it applies (winsize 9, else k_flow_scan)
     PolyCoef pc;
     // getStructuringElement(MORPH_ELLIPSE, (mk, mk)) (of:62), anchor (mk/2, mk/2):
     // element row i (dy = i - mk/2) covers dx = mlo[i] .. mhi[i] (empty if
@@ -135,8 +136,10 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
                              size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s);
 // Farneback levels k_hi down to k_lo (L..0 in total, coarse to fine) for frames
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
+// `kernel` (nullable): which flow kernel the launches of level k_lo took —
+// DVC_KTIME_FLOW (k_flow, direct sums), DVC_KTIME_FLOW_SCAN, DVC_KTIME_FLOW_SCAN2
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0 = nullptr);
+                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0 = nullptr, int* kernel = nullptr);
 // hand-off slots (16 B each) k_flow_scan needs per frame at a level of w x h
 size_t of_scan_slots(const OfGeom& g, int w, int h);
 // vote (frames in order) -> close/open -> 8-CC bounding boxes -> rectangle mask

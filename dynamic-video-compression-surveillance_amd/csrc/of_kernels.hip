@@ -1540,7 +1540,7 @@ __device__ unsigned long long g_scan2_stamps[32 * 96 * 8];
 // items and run the same barriers; split at the top so that no value of one
 // role is live in the other's code.
 template <int SMODE, bool CHAIN>
-__device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float* tb0, int& s_item, int& s_alive)
+__device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float* tb0, int& s_item, int* s_alive)
 {
     using namespace scan2;
     const FlowArgs& A = S.f;
@@ -1555,13 +1555,21 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
         const int q = (int)((blockIdx.x + kq) % SCAN_Q);
         const int total = q < n ? ((n - 1 - q) / SCAN_Q + 1) * S.S : 0;
         for (;;) {
-            if (tid == 0) {
-                s_item = (int)atomicAdd(S.next + q, 1u);
-                s_alive = 1;
-            }
+            if (tid == 0) s_item = (int)atomicAdd(S.next + q, 1u);
             __syncthreads();
             const int it = s_item;
             __syncthreads();
+            // the abort flags of the item: s_alive[k & 1] is written (0) only in
+            // interval k, by the chain wave, and read by every wave right after
+            // interval k's barrier; the chain wave reaches interval k + 2 (the
+            // next write of that flag) only after barrier k + 1, which every M
+            // wave passes after its read. Reset here, after the item-start
+            // barriers: every read of the previous item's flags came before them
+            // (one flag let a wave see interval k+1's abort at k)
+            if (tid == 0) {
+                s_alive[0] = 1;
+                s_alive[1] = 1;
+            }
             if (it >= total) break;
             const int t = q + SCAN_Q * (it / S.S), s = it % S.S;
             const int X0 = s * SW, X1 = min(X0 + SW, w), CX0 = X0 - M - 1, nx = X1 - X0;
@@ -1589,7 +1597,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                         // (lanes 60..63 poll lane 59's slot: they run its chain and
                         // store the same values to the same words)
                         if (s > 0 && li < nrow * 5 && !scan_poll(S, r_left, (uint32_t)(k * 64 + li) * 16u, acc))
-                            s_alive = 0;
+                            s_alive[k & 1] = 0;
                         // line (i, c) of the block's sum buffer; column x' = x - CX0
                         double* v = sv0 + (size_t)(k % 3) * SVB + (li / 5) * 5 * P + (li % 5) * P;
                         if (s == 0) {   // OpenCV's start: vsum[0] (m+2) + vsum[1..m-1] (x' = x + m + 1)
@@ -1643,7 +1651,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                     if (lane == 0) STAMP2(t, k, 2);
                     __syncthreads();
                     if (lane == 0) STAMP2(t, k, 3);
-                    if (!s_alive) break;   // uniform: read after the barrier
+                    if (!s_alive[k & 1]) break;   // uniform: interval k's flag, read after its barrier
                 }
                 __builtin_amdgcn_s_setprio(0);
                 continue;
@@ -1803,7 +1811,7 @@ __device__ __forceinline__ void scan2_role(const ScanArgs& S, double* sv0, float
                 if (!DVC_STAMP_DETAIL && tid == 640) STAMP2(t, k, 6);   // wave 10 (S + G)
                 if (tid == (DVC_STAMP_DETAIL ? 640 : 960)) STAMP2(t, k, 7);   // wave 15 (S + G) / wave 10
                 __syncthreads();
-                return s_alive != 0;
+                return s_alive[k & 1] != 0;   // interval k's flag (k = -1: parity 1, never written)
             };
             // k = -1: X = G(1)'s set (PB), Y = G(2)'s (PA)
             for (int k = -1; k <= NB; k += 2) {
@@ -1821,7 +1829,7 @@ __global__ void __launch_bounds__(1024, 1) k_flow_scan2(ScanArgs S)
     extern __shared__ __attribute__((aligned(16))) double lds_s2[];
     double* sv0 = lds_s2;                                             // 3 sum buffers
     float* tb0 = reinterpret_cast<float*>(lds_s2 + 3 * scan2::SVB);   // 2 transfer buffers
-    __shared__ int s_item, s_alive;
+    __shared__ int s_item, s_alive[2];
     if (threadIdx.x < 64) scan2_role<SMODE, true>(S, sv0, tb0, s_item, s_alive);
     else scan2_role<SMODE, false>(S, sv0, tb0, s_item, s_alive);
 }
@@ -2538,7 +2546,7 @@ size_t of_scan_slots(const OfGeom& g, int w, int h)
 }
 
 hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, long long a0, int n, int k_hi, int k_lo,
-                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0)
+                          hipStream_t s, unsigned int* epoch, hipEvent_t ev_it0, int* kernel)
 {
     a0 = reduce_frame(g, a0);
     static const int cus = [] {
@@ -2604,9 +2612,11 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                     S.f.src = up;
                 }
                 // the pipelined scan for the reference's winsize 9 (m == 4);
-                // DVC_OF_SCAN2=0 selects the barrier-phased k_flow_scan (A/B)
-                static const int scan2_env = [] { const char* e = getenv("DVC_OF_SCAN2"); return e ? atoi(e) : 1; }();
-                if (g.m == scan2::M && rb == scan2::RB && scan2_env) {
+                // g.sliding == 1 (DVC_OF_SCAN2=0 at create) selects the
+                // barrier-phased k_flow_scan
+                const bool use2 = g.m == scan2::M && rb == scan2::RB && g.sliding == 2;
+                if (kernel && k == k_lo) *kernel = use2 ? DVC_KTIME_FLOW_SCAN2 : DVC_KTIME_FLOW_SCAN;
+                if (use2) {
                     const int items = S.S * n, grid_s = std::max(1, std::min(items, cus));
                     if (S.f.src_mode == 2)
                         hipLaunchKernelGGL(k_flow_scan2<2>, dim3(grid_s), dim3(scan2::NT), scan2::LDS, s, S);
@@ -2643,8 +2653,10 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
 #undef DVC_SCAN_CASE
                 }
             } else if (g.m == 4) {
+                if (kernel && k == k_lo) *kernel = DVC_KTIME_FLOW;
                 hipLaunchKernelGGL(k_flow<4>, grid, dim3(256), lds, s, A);
             } else {
+                if (kernel && k == k_lo) *kernel = DVC_KTIME_FLOW;
                 hipLaunchKernelGGL(k_flow<0>, grid, dim3(256), lds, s, A);
             }
             if (ev_it0 && k == k_lo && it == 0) {   // the caller schedules other work after it

@@ -177,6 +177,17 @@ class OFWorker:
         N.check(self._lib.dvc_of_ktime(self._h, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0))
         return float(ms.value), int(n.value)
 
+    def ktime_kernel(self) -> str:
+        """The kernel that ran the level-0 iterations of the last batch (what
+        :meth:`ktime` timed): "k_flow" (direct sums), "k_flow_scan" (the
+        barrier-phased running-sum scan) or "k_flow_scan2" (the pipelined scan)."""
+        if not hasattr(self._lib, "dvc_of_ktime_kernel"):   # an older build (DVC_LIB_PATH A/B)
+            return "k_flow_scan2"
+        k = self._lib.dvc_of_ktime_kernel(self._h)
+        if k < 0:
+            N.check(k)
+        return {N.KTIME_FLOW: "k_flow", N.KTIME_FLOW_SCAN: "k_flow_scan", N.KTIME_FLOW_SCAN2: "k_flow_scan2"}[k]
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.dvc_of_destroy(self._h)

@@ -406,6 +406,16 @@ int dvc_of_read_flow(dvc_of* h, float* host_dst);
  * Farneback iterations (k_flow at level 0, the dominant kernel). */
 int dvc_of_ktime(dvc_of* h, double* total_ms, uint64_t* launches, int reset);
 
+/* Which kernel ran the level-0 Farneback iterations of the last batch (what
+ * dvc_of_ktime timed): DVC_KTIME_FLOW (k_flow: DVC_FLAG_OF_DIRECT_SUMS),
+ * DVC_KTIME_FLOW_SCAN (the barrier-phased running-sum scan: winsize other than
+ * 9) or DVC_KTIME_FLOW_SCAN2 (the pipelined scan, the reference's winsize 9).
+ * Negative on error (DVC_E_STATE before the first step). */
+#define DVC_KTIME_FLOW 2
+#define DVC_KTIME_FLOW_SCAN 3
+#define DVC_KTIME_FLOW_SCAN2 4
+int dvc_of_ktime_kernel(const dvc_of* h);
+
 void dvc_of_destroy(dvc_of* h);
 
 /* Parity/debug readback of Farneback intermediates of the LAST stepped frame at

@@ -107,7 +107,7 @@ def test_of_parity_synthetic(gpu_lib, oracle_lib, W, H, n, seed, noisy):
 
 @pytest.mark.parametrize("direct", [False, True])
 def test_of_parity_1080p(gpu_lib, oracle_lib, direct):
-    """Both box-sum orders: OpenCV's running sums (k_flow_scan, the default) and
+    """Both box-sum orders: OpenCV's running sums (k_flow_scan2, the default) and
     direct per-pixel sums (k_flow, DVC_FLAG_OF_DIRECT_SUMS), each vs the oracle
     computing the same order."""
     from dvc_amd.synthetic import clip
@@ -369,3 +369,84 @@ def test_of_upsample_forms_agree(gpu_lib, oracle_lib, W, H, monkeypatch):
             assert np.array_equal(f.view(np.uint32), rflows[t - 1].view(np.uint32)), \
                 f"gather={gather} rows={rows}: flow differs at frame {t}: {_first_diff(f, rflows[t - 1])}"
         gpu.close()
+
+
+@pytest.mark.parametrize("W,H,n,batch", [(333, 185, 5, 0), (1920, 1080, 3, 2)])
+def test_of_scan_forms_agree(gpu_lib, oracle_lib, W, H, n, batch, monkeypatch):
+    """The pipelined k_flow_scan2 (the default for winsize 9) and the
+    barrier-phased k_flow_scan it replaced (DVC_OF_SCAN2=0 at create: the
+    form winsize != 9 takes) give the same flow bits, masks and compressed
+    frames — a partial last strip (333 px) and a height that is not a multiple
+    of the 12-row blocks (185, 1080 / 2^k) — and the library reports which one
+    ran (dvc_of_ktime_kernel). At 333 x 185 both also equal the oracle."""
+    from dvc_amd.synthetic import clip
+    frames = clip(W, H, n, seed=W + H)
+    runs = {}
+    for scan2 in ("1", "0"):
+        monkeypatch.setenv("DVC_OF_SCAN2", scan2)
+        gpu = gpu_lib.OFWorker(W, H, keep_planes=True, max_batch=max(batch, 1))
+        gpu.prime(frames[0])
+        if batch:
+            masks, cps = gpu.step_batch(frames[1:])
+            runs[scan2] = ([gpu.flow()], list(masks), list(cps), gpu.stats())
+        else:
+            fl, ms, cs = [], [], []
+            for t in range(1, n):
+                m, c = gpu.step(frames[t])
+                fl.append(gpu.flow())
+                ms.append(m)
+                cs.append(c)
+            runs[scan2] = (fl, ms, cs, gpu.stats())
+        assert gpu.ktime_kernel() == ("k_flow_scan2" if scan2 == "1" else "k_flow_scan")
+        gpu.close()
+    a, b = runs["1"], runs["0"]
+    for k, (fa, fb) in enumerate(zip(a[0], b[0])):
+        assert np.array_equal(fa.view(np.uint32), fb.view(np.uint32)), f"flow differs (step {k}): {_first_diff(fa, fb)}"
+    for t, (ma, mb) in enumerate(zip(a[1], b[1])):
+        assert np.array_equal(ma, mb), f"mask differs at frame {t + 1}"
+    for t, (ca, cb) in enumerate(zip(a[2], b[2])):
+        assert np.array_equal(ca, cb), f"compressed differs at frame {t + 1}"
+    assert a[3] == b[3]
+    if not batch:
+        ref = oracle_lib.OracleOF(W, H)
+        ref.prime(frames[0])
+        for t in range(1, n):
+            rm, rc, rf = ref.step(frames[t])
+            assert np.array_equal(a[0][t - 1].view(np.uint32), rf.view(np.uint32)), f"flow vs oracle, frame {t}"
+            assert np.array_equal(a[1][t - 1], rm) and np.array_equal(a[2][t - 1], rc), f"outputs vs oracle, frame {t}"
+        ref.close()
+
+
+@pytest.mark.parametrize("scan2", ["1", "0"])
+def test_of_scan_abort_drains(gpu_lib, oracle_lib, scan2, monkeypatch):
+    """A strip hand-off wait that fails (fault injection: DVC_OF_FAULT=scan_abort
+    raises the abort flag before every batch, the path a ~1 s poll timeout
+    takes) drains the launch — every wave of a workgroup leaves the interval
+    loop at the same barrier — and the error comes back from the
+    call instead of a hang. A handle created afterwards runs bit-exact."""
+    import time
+    from dvc_amd._native import DVC_E_HIP, DvcError
+    from dvc_amd.synthetic import clip
+    W, H = 1920, 1080
+    frames = clip(W, H, 5, seed=9)
+    monkeypatch.setenv("DVC_OF_SCAN2", scan2)
+    monkeypatch.setenv("DVC_OF_FAULT", "scan_abort")
+    gpu = gpu_lib.OFWorker(W, H, max_batch=4)
+    gpu.prime(frames[0])
+    t0 = time.perf_counter()
+    with pytest.raises(DvcError) as ei:
+        gpu.step_batch(frames[1:])
+    assert ei.value.code == DVC_E_HIP and "hand-off" in str(ei.value)
+    assert time.perf_counter() - t0 < 20.0
+    gpu.close()
+    monkeypatch.delenv("DVC_OF_FAULT")
+    gpu = gpu_lib.OFWorker(W, H, keep_planes=True)
+    ref = oracle_lib.OracleOF(W, H)
+    gpu.prime(frames[0])
+    ref.prime(frames[0])
+    m, c = gpu.step(frames[1])
+    rm, rc, rf = ref.step(frames[1])
+    assert np.array_equal(gpu.flow().view(np.uint32), rf.view(np.uint32))
+    assert np.array_equal(m, rm) and np.array_equal(c, rc)
+    gpu.close()
+    ref.close()
