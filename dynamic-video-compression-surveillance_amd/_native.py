@@ -48,6 +48,7 @@ EXPORTS = [
     "dvc_of_debug_read", "dvc_host_alloc", "dvc_host_free", "dvc_yuv420_to_bgr", "dvc_bgr_to_i420",
     "dvc_copy_rate", "dvc_ofc_create", "dvc_ofc_run", "dvc_ofc_sync", "dvc_ofc_destroy",
     "dvc_fd_set_state", "dvc_of_set_state", "dvc_fd_ktime_kernel", "dvc_of_ktime_kernel",
+    "dvc_fd_graph_stats",
 ]
 ABI_VERSION = 7
 MAX_BATCH = 512
@@ -178,6 +179,9 @@ def lib() -> ctypes.CDLL:
     if hasattr(L, "dvc_fd_ktime_kernel"):   # (an older build under DVC_LIB_PATH lacks it)
         L.dvc_fd_ktime_kernel.argtypes = [vp]
         L.dvc_fd_ktime_kernel.restype = ctypes.c_int
+    if hasattr(L, "dvc_fd_graph_stats"):
+        L.dvc_fd_graph_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.dvc_fd_graph_stats.restype = ctypes.c_int
     if hasattr(L, "dvc_of_ktime_kernel"):
         L.dvc_of_ktime_kernel.argtypes = [vp]
         L.dvc_of_ktime_kernel.restype = ctypes.c_int

@@ -19,8 +19,10 @@
 #include "../../include/dvc.h"
 #include "dct_const.h"
 #include "fd_kernels.h"
+#include "klaunch.h"
 #include "host_common.h"
 #include "yuv_kernels.h"
+#include "tune.h"
 
 namespace dvc_host {
 
@@ -117,6 +119,22 @@ int gauss_taps(int n, double sigma, uint16_t* taps)
 
 }  // namespace
 
+// One batch's launch sequence as a HIP graph (enqueue_batch's graph path, VERDICT
+// r5 #4): the launches of the four stages as dvc::klaunch recorded them, one
+// chain in stage order, with event nodes for the recurrences across batches
+// (wait for the previous batch's stage, record this batch's). A later batch of
+// the same launch shape re-uses it with the arguments that changed set in place.
+struct FdGraph {
+    std::vector<dvc::KNode> rec[4];          // front, contour filter, accumulate, output: arguments as set in ge
+    std::vector<hipGraphNode_t> node[4];
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    uint64_t used = 0;                       // seq of its last launch (least recently used is replaced)
+};
+constexpr int NGRAPH = 4;                    // graphs kept per slot (launch shapes: frame count, outputs, format)
+constexpr int GRAPH_MAX_FRAMES = 32;         // batches up to this many frames take the graph path (the
+                                             // drop-in's read-ahead; each slot's own filter set holds as many)
+
 // Buffers of one batch in flight (max_batch frames): motion masks, contour-
 // filter scratch, kept masks, the dilate -> accumulate -> out bits, and the
 // staged input frames when the caller's cannot be read in place.
@@ -133,10 +151,20 @@ struct Slot {
     // when not requested): a fused front writes outputs before the previous
     // batches' k_fix4 have run, so it waits for those that write the same bytes
     uintptr_t olo[2] = {0, 0}, ohi[2] = {0, 0};
+    bool graph = false;     // its last batch ran as a graph: only ev_front, ev_acc, ev_out were recorded
+    std::vector<FdGraph> graphs;   // the graph path's graphs of this slot's batches
+    // the graph path's contour filter: the slot's own working set (S.c's
+    // mbits / kbits / kocc with its own run index, parents, areas, filled
+    // bits), so consecutive batches' filters overlap instead of queueing on
+    // one shared set; allocated at the slot's first graph batch
+    dvc::CclBufs gc{};
+    std::vector<void*> gc_mem;
 };
 
-// Batches in flight: three slots.
-constexpr int NSLOT = 3;
+// Batches in flight: four slots (the graph path launches each slot's batches
+// on its own stream, so up to four short batches overlap; the stage streams
+// keep the four stages of four batches in flight).
+constexpr int NSLOT = 4;
 
 // Host-pointer path: two staging sets, so chunk c+1's frames go up while chunk
 // c computes and chunk c-1's outputs come down.
@@ -205,7 +233,18 @@ struct dvc_fd {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     bool last_fused = false;   // the last batch ran the fused front (KTIMING timed k_front, not k_out)
+    bool graph_ok = true;      // short device-frame batches take the graph path (DVC_FD_GRAPH=0 at create: never)
+    bool prev_graph = false;   // the last batch ran as a graph (its stages ran on its slot's graph stream)
+    uint64_t graph_batches = 0, graph_builds = 0;   // batches launched as graphs, graphs built (dvc_fd_graph_stats)
 };
+
+// The stream a slot's graphs are launched on: one of the handle's four streams
+// per slot (each its own hardware queue at the default 4), so consecutive
+// batches' graphs overlap — batch i's contour filter beside batch i+1's front
+static hipStream_t graph_stream(dvc_fd* h, int k)
+{
+    return k == 0 ? h->stream : k == 1 ? h->s_acc : k == 2 ? h->s_out : h->s_front;
+}
 
 static void free_all(dvc_fd* h)
 {
@@ -222,6 +261,13 @@ static void free_all(dvc_fd* h)
         }
         for (hipEvent_t e : {s.ev_front, s.ev_ccl, s.ev_acc, s.ev_out})
             if (e) (void)hipEventDestroy(e);
+        for (FdGraph& G : s.graphs) {
+            if (G.ge) (void)hipGraphExecDestroy(G.ge);
+            if (G.g) (void)hipGraphDestroy(G.g);
+        }
+        s.graphs.clear();
+        for (void* p : s.gc_mem) (void)hipFree(p);
+        s.gc_mem.clear();
     }
     for (Stage& s : h->stage) {
         for (void* p : {(void*)s.d_in, (void*)s.d_ov, (void*)s.d_cp})
@@ -310,7 +356,7 @@ static bool direct_frames(const dvc_fd* h, const uint8_t* p, size_t pitch, size_
 // DVC_FD_YUV_DIRECT=0 forces the staged conversion (A/B).
 static bool direct_yuv(const dvc_fd* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
-    static const int on = [] { const char* e = getenv("DVC_FD_YUV_DIRECT"); return e ? atoi(e) : 1; }();
+    static const int on = [] { const char* e = dvc::tune_env("DVC_FD_YUV_DIRECT"); return e ? atoi(e) : 1; }();
     return on && h->fmt != DVC_FMT_BGR && !h->resize && h->p.width % 4 == 0 && pitch % 4 == 0 &&
            ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
@@ -464,6 +510,9 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     {   // DVC_FD_FUSED8=1 (read per handle): the fused front for block_size 8 (see enqueue_batch)
         const char* e = getenv("DVC_FD_FUSED8");
         h->fused8 = e && atoi(e) != 0;
+        // DVC_FD_GRAPH=0 (read per handle): every batch on the stage streams (tests compare both paths)
+        const char* g = getenv("DVC_FD_GRAPH");
+        h->graph_ok = !g || atoi(g) != 0;
     }
     h->ofb = (p.flags & DVC_FLAG_OUT_I420) ? (size_t)p.width * p.height * 3 / 2 : (size_t)p.width * p.height * 3;
     h->crows = p.chroma_rows ? p.chroma_rows : h->sh;
@@ -503,7 +552,7 @@ int dvc_fd_create(const dvc_fd_params* prm, int device, void* hip_stream, dvc_fd
     (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
     // priorities of the front, contour-filter, accumulate and output streams:
     // 'l'ow, 'n'ormal, 'h'igh; DVC_PRIO overrides for sweeps (default "lnnh")
-    static const char* prio = [] { const char* e = getenv("DVC_PRIO"); return e && strlen(e) == 4 ? e : "lnnh"; }();
+    static const char* prio = [] { const char* e = dvc::tune_env("DVC_PRIO"); return e && strlen(e) == 4 ? e : "lnnh"; }();
     auto level = [&](char c) { return c == 'l' ? plo : c == 'h' ? phi : 0; };
     auto mk = [](hipStream_t* st, int pr) { return hipStreamCreateWithPriority(st, hipStreamNonBlocking, pr); };
     if ((e = mk(&h->stream, level(prio[1]))) != hipSuccess) return bad(e, "hipStreamCreate");
@@ -764,6 +813,7 @@ int dvc_fd_prime(dvc_fd* h, const uint8_t* bgr, size_t pitch)
     h->primed = true;
     h->failed = false;
     h->err_frame = 0;
+    h->prev_graph = false;
     return DVC_OK;
 }
 
@@ -793,10 +843,145 @@ int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
     h->primed = true;
     h->failed = false;
     h->err_frame = 0;
+    h->prev_graph = false;
     return DVC_OK;
 }
 
 }  // extern "C"
+
+// The graph path of one batch (device frames read in place, <= GRAPH_MAX_FRAMES
+// frames, no KTIMING): the four stages' launches are recorded (dvc::klaunch),
+// matched against this slot's graphs by launch shape and launched as one
+// graph on the slot's graph stream. A call then costs one graph launch and a
+// few argument updates instead of nine launches and eleven event operations
+// across four streams (~80 us of host time a call, profiles/r6_fd_per_call_*).
+// Chain: [wait P.front] front [rec S.front] contour filter [rec S.ccl]
+// [wait P.acc] dilate, accumulate [rec S.acc] outputs [rec S.out], P = the
+// previous batch's slot — the recurrences the stage streams give the direct
+// path (previous gray, accumulated mask); the contour filter runs on the
+// slot's own working set (graph_ccl), so it needs no order across batches. Before the launch, on the graph stream: the slot's
+// previous batch (S.out: every buffer of the slot is free) and `wait_out`
+// (earlier batches whose outputs the fused front overwrites).
+// The slot's own contour-filter working set for graph batches (Slot::gc), for
+// min(max_batch, GRAPH_MAX_FRAMES) frames: ~17 MB a 1080p frame.
+static int graph_ccl(dvc_fd* h, Slot& S)
+{
+    if (!S.gc_mem.empty()) return DVC_OK;
+    const int gmb = std::min(h->max_batch, GRAPH_MAX_FRAMES);
+    size_t sz[dvc::CclBufs::NARR];
+    dvc::CclBufs::sizes(h->g, gmb, sz);
+    S.gc = S.c;
+    void** ptrs[dvc::CclBufs::NARR];
+    S.gc.ptrs(ptrs);
+    for (int i = 0; i < dvc::CclBufs::NARR; ++i) {
+        if (!dvc::CclBufs::working_set(i)) continue;
+        void* p = nullptr;
+        const hipError_t e = hipMalloc(&p, sz[i] ? sz[i] : 16);
+        if (e != hipSuccess) {
+            for (void* q : S.gc_mem) (void)hipFree(q);
+            S.gc_mem.clear();
+            return fail(e == hipErrorOutOfMemory ? DVC_E_NOMEM : DVC_E_HIP, "graph contour-filter set: %s",
+                        hipGetErrorString(e));
+        }
+        S.gc_mem.push_back(p);
+        *ptrs[i] = p;
+    }
+    // every frame slice's OUTSIDE gap node is its own root before any k_band (as at create)
+    HIP_OK(hipMemsetAsync(S.gc.gpar, 0, sz[6], graph_stream(h, (int)(&S - h->slot))));
+    return DVC_OK;
+}
+
+static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], const std::vector<hipEvent_t>& wait_out)
+{
+    const int k = (int)(h->seq % NSLOT);
+    Slot& P = h->slot[(h->seq + NSLOT - 1) % NSLOT];
+    hipStream_t z = graph_stream(h, k);
+    FdGraph* G = nullptr;
+    for (FdGraph& x : S.graphs) {
+        bool same = true;
+        for (int sg = 0; sg < 4 && same; ++sg) {
+            same = x.rec[sg].size() == rec[sg].size();
+            for (size_t u = 0; same && u < rec[sg].size(); ++u) same = x.rec[sg][u].same_shape(rec[sg][u]);
+        }
+        if (same) {
+            G = &x;
+            break;
+        }
+    }
+    std::vector<void*> pp;
+    if (G) {
+        // the exec's previous launch (batch i-3, this slot's) must have read its
+        // arguments before they are overwritten: wait for it on the host (it is
+        // three batches back, so the device keeps two batches queued meanwhile)
+        if (S.recorded) HIP_OK(hipEventSynchronize(S.ev_out));
+        for (int sg = 0; sg < 4; ++sg)
+            for (size_t u = 0; u < rec[sg].size(); ++u) {
+                dvc::KNode& cur = G->rec[sg][u];
+                if (cur.args == rec[sg][u].args) continue;
+                cur.args.swap(rec[sg][u].args);
+                hipKernelNodeParams kp{};
+                kp.func = const_cast<void*>(cur.f);
+                kp.gridDim = cur.grid;
+                kp.blockDim = cur.block;
+                kp.sharedMemBytes = cur.shm;
+                cur.params(pp);
+                kp.kernelParams = pp.data();
+                HIP_OK(hipGraphExecKernelNodeSetParams(G->ge, G->node[sg][u], &kp));
+            }
+    } else {
+        if ((int)S.graphs.size() >= NGRAPH) {   // replace the least recently used one
+            size_t lru = 0;
+            for (size_t u = 1; u < S.graphs.size(); ++u)
+                if (S.graphs[u].used < S.graphs[lru].used) lru = u;
+            if (S.recorded) HIP_OK(hipEventSynchronize(S.ev_out));
+            (void)hipGraphExecDestroy(S.graphs[lru].ge);
+            (void)hipGraphDestroy(S.graphs[lru].g);
+            S.graphs.erase(S.graphs.begin() + (long)lru);
+        }
+        S.graphs.emplace_back();
+        G = &S.graphs.back();
+        HIP_OK(hipGraphCreate(&G->g, 0));
+        // (no wait for the previous batch's contour filter: the slot has its own
+        // working set; no record of this one's: Slot::graph — an event node costs
+        // ~5 us of the chain's latency on the device)
+        const hipEvent_t waits[4] = {P.ev_front, nullptr, P.ev_acc, nullptr};
+        const hipEvent_t recs[4] = {S.ev_front, nullptr, S.ev_acc, S.ev_out};
+        hipGraphNode_t last = nullptr;   // one chain: every node depends on the one before
+        auto dep = [&]() { return last ? 1u : 0u; };
+        for (int sg = 0; sg < 4; ++sg) {
+            hipGraphNode_t nd = nullptr;
+            if (waits[sg]) {
+                HIP_OK(hipGraphAddEventWaitNode(&nd, G->g, last ? &last : nullptr, dep(), waits[sg]));
+                last = nd;
+            }
+            for (dvc::KNode& kn : rec[sg]) {
+                hipKernelNodeParams kp{};
+                kp.func = const_cast<void*>(kn.f);
+                kp.gridDim = kn.grid;
+                kp.blockDim = kn.block;
+                kp.sharedMemBytes = kn.shm;
+                kn.params(pp);
+                kp.kernelParams = pp.data();
+                HIP_OK(hipGraphAddKernelNode(&nd, G->g, last ? &last : nullptr, dep(), &kp));
+                G->node[sg].push_back(nd);
+                last = nd;
+            }
+            if (recs[sg]) {
+                HIP_OK(hipGraphAddEventRecordNode(&nd, G->g, last ? &last : nullptr, dep(), recs[sg]));
+                last = nd;
+            }
+            G->rec[sg].swap(rec[sg]);
+        }
+        HIP_OK(hipGraphInstantiate(&G->ge, G->g, nullptr, nullptr, 0));
+        h->graph_builds++;
+    }
+    if (S.recorded) HIP_OK(hipStreamWaitEvent(z, S.ev_out, 0));
+    for (hipEvent_t e : wait_out) HIP_OK(hipStreamWaitEvent(z, e, 0));
+    HIP_OK(hipGraphLaunch(G->ge, z));
+    G->used = h->seq;
+    h->graph_batches++;
+    return DVC_OK;
+}
 
 // Enqueue one batch i of n <= max_batch frames, slot S = i % 3 (j = i - 3 =
 // the slot's previous batch):
@@ -808,7 +993,9 @@ int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
 //   s_out:           [wait ev_acc]            k_out(i), or k_out_gen + k_fix4(i) when fused -> ev_out
 // so front(i+2), the contour filter of i+1, the accumulation of i and the
 // output of i-1 can all be in flight; the two recurrences (previous gray,
-// accumulated mask) are serial, each on its own stream.
+// accumulated mask) are serial, each on its own stream. Short batches of
+// device frames take the graph path instead (enqueue_graph): the same
+// kernels, arguments and dependencies.
 static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride, int crows)
 {
@@ -828,7 +1015,22 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
 #else
     constexpr int skip = 0;
 #endif
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_ccl, 0));
+    const bool timed = h->p.flags & DVC_FLAG_KTIMING;
+    // the graph path: device frames the kernels read in place (no staging
+    // launches), short batches; DVC_FD_GRAPH=0 at create turns it off
+    const bool graph = h->graph_ok && (h->p.flags & DVC_FLAG_DEVICE_PTRS) && !timed && !skip &&
+                       n <= GRAPH_MAX_FRAMES &&
+                       (direct_frames(h, src, pitch, fstride, n) || direct_yuv(h, src, pitch, fstride, n));
+    if (!graph && h->prev_graph) {
+        // the previous batch ran on its slot's graph stream: the stage streams
+        // take its recurrences from its events
+        const Slot& P = h->slot[(h->seq + NSLOT - 1) % NSLOT];
+        HIP_OK(hipStreamWaitEvent(h->s_front, P.ev_front, 0));
+        HIP_OK(hipStreamWaitEvent(s_ccl, P.ev_out, 0));   // (a graph batch records no ev_ccl)
+        HIP_OK(hipStreamWaitEvent(h->s_acc, P.ev_acc, 0));
+        HIP_OK(hipStreamWaitEvent(h->s_out, P.ev_out, 0));
+    }
+    if (S.recorded && !graph) HIP_OK(hipStreamWaitEvent(h->s_front, S.graph ? S.ev_out : S.ev_ccl, 0));
     const uint8_t* d = nullptr;
     int dp = 0;
     size_t dfs = 0;
@@ -842,7 +1044,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     // surfaces read in place (or staged), BGR outputs in dword rows or I420
     // frames (DVC_FLAG_OUT_I420: the front and k_fix4 write BGR2YUV_I420);
     // DVC_FD_FUSED=0 turns it off (A/B)
-    static const int fuse_env = [] { const char* e = getenv("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
+    static const int fuse_env = [] { const char* e = dvc::tune_env("DVC_FD_FUSED"); return e ? atoi(e) : 1; }();
     // (B = 4: k_fix4 scans a block row's static words in one wave, SW <= 64;
     // B = 8, opt-in with DVC_FD_FUSED8=1: BGR frames, fixed up by k_out<8>'s
     // per-block pass. Not the default: the 8x8 DCT at four lanes a block makes
@@ -859,12 +1061,13 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         S.ohi[1] = cp ? (uintptr_t)cp + span : 0;
     }
     dvc::FrontOut fo{};
+    std::vector<hipEvent_t> wait_out;   // fused: earlier batches whose outputs this one's front overwrites
     if (fused) {
         // the speculative stores must not land before an earlier batch's k_fix4
         // rewrites the same bytes: wait for the slot's previous batch (so every
         // k_fix4 up to batch i-3 is done, s_out being in order) and for batches
         // i-1, i-2 where their outputs overlap this one's
-        if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
+        if (S.recorded && !graph) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
         for (int k = 1; k < NSLOT; ++k) {
             const Slot& P = h->slot[(h->seq + NSLOT - k) % NSLOT];
             if (!P.recorded) continue;
@@ -873,8 +1076,10 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
                 for (int v = 0; v < 2; ++v)
                     overlap = overlap || (S.ohi[u] > S.olo[u] && P.ohi[v] > P.olo[v] && S.olo[u] < P.ohi[v] &&
                                           P.olo[v] < S.ohi[u]);
-            if (overlap) HIP_OK(hipStreamWaitEvent(h->s_front, P.ev_out, 0));
+            if (overlap) wait_out.push_back(P.ev_out);
         }
+        if (!graph)
+            for (hipEvent_t e : wait_out) HIP_OK(hipStreamWaitEvent(h->s_front, e, 0));
         fo.ov = ov;
         fo.cp = cp;
         fo.opitch = opitch;
@@ -885,33 +1090,6 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         fo.B = h->B;
         fo.i420 = out_i420 ? 1 : 0;
     }
-    // KTIMING: events around the dominant HBM kernel — the fused front on
-    // s_front, else k_out on s_out
-    const bool timed = h->p.flags & DVC_FLAG_KTIMING;
-    if (timed) {
-        while (h->ev.size() < h->ev_used + 2) {
-            hipEvent_t e;
-            HIP_OK(hipEventCreate(&e));
-            h->ev.push_back(e);
-        }
-    }
-    if (timed && fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_front));
-    if (!(skip & 1))
-        HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
-                                 h->p.ithresh, h->s_front, fused ? &fo : nullptr));
-    if (timed && fused) {
-        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_front));
-        h->ev_used += 2;
-    }
-    h->last_fused = fused;
-    HIP_OK(hipEventRecord(S.ev_front, h->s_front));
-    h->gcur ^= 1;
-    HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_front, 0));
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_acc, 0));
-    if (!(skip & 2)) HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, s_ccl));
-    HIP_OK(hipEventRecord(S.ev_ccl, s_ccl));
-    HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_ccl, 0));
-    if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_out, 0));
     dvc::BackArgs a{};
     a.g = h->g;
     a.bgr = d;
@@ -952,7 +1130,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         const float z = std::rint(std::fmaf(0.0f, h->p.alpha, std::fmaf(0.0f, h->p.beta, h->p.gamma)));
         a.acc0_fixed = z < 0.5f && z > -0.5f;  // saturate_cast<uchar>(0) == 0 (NaN/negatives excluded)
         const float dil1 = std::fmaf(255.0f, h->p.beta, h->p.gamma);
-        static const bool acc_general = getenv("DVC_ACC_GENERAL") != nullptr;  // A/B: the general form always
+        static const bool acc_general = dvc::tune_env("DVC_ACC_GENERAL") != nullptr;  // A/B: the general form always
         a.acc_fast = dvc::acc_fast_ok(h->p.alpha, h->p.beta, h->p.gamma) && !acc_general;
         std::memcpy(&a.dil1_bits, &dil1, 4);
     }
@@ -962,16 +1140,67 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     a.dbg_dil = h->dbg_dil;
     a.err = h->err;
     a.frame0 = h->frames;
-    if (!(skip & 4)) HIP_OK(dvc::launch_accumulate(a, h->s_acc));
-    HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
-    HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
-    if (timed && !fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
-    if (!(skip & 8)) HIP_OK(dvc::launch_out(a, h->s_out, fused));
-    if (timed && !fused) {
-        HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
-        h->ev_used += 2;
+    h->last_fused = fused;
+    if (graph) {
+        std::vector<dvc::KNode> rec[4];
+        hipError_t e[4];
+        hipStream_t z = graph_stream(h, (int)(h->seq % NSLOT));
+        rc = graph_ccl(h, S);
+        if (rc) return rc;
+        dvc::g_krec = &rec[0];
+        e[0] = dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
+                                 h->p.ithresh, z, fused ? &fo : nullptr);
+        dvc::g_krec = &rec[1];
+        e[1] = dvc::launch_ccl(S.gc, h->g, n, h->p.min_area2, z);
+        dvc::g_krec = &rec[2];
+        e[2] = dvc::launch_accumulate(a, z);
+        dvc::g_krec = &rec[3];
+        e[3] = dvc::launch_out(a, z, fused);
+        dvc::g_krec = nullptr;
+        for (hipError_t x : e) HIP_OK(x);
+        rc = enqueue_graph(h, S, rec, wait_out);
+        if (rc) return rc;
+        h->prev_graph = true;
+        S.graph = true;
+    } else {
+        // KTIMING: events around the dominant HBM kernel — the fused front on
+        // s_front, else k_out on s_out
+        if (timed) {
+            while (h->ev.size() < h->ev_used + 2) {
+                hipEvent_t e;
+                HIP_OK(hipEventCreate(&e));
+                h->ev.push_back(e);
+            }
+        }
+        if (timed && fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_front));
+        if (!(skip & 1))
+            HIP_OK(dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
+                                     h->p.ithresh, h->s_front, fused ? &fo : nullptr));
+        if (timed && fused) {
+            HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_front));
+            h->ev_used += 2;
+        }
+        HIP_OK(hipEventRecord(S.ev_front, h->s_front));
+        HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_front, 0));
+        if (S.recorded) HIP_OK(hipStreamWaitEvent(s_ccl, S.ev_acc, 0));
+        if (!(skip & 2)) HIP_OK(dvc::launch_ccl(S.c, h->g, n, h->p.min_area2, s_ccl));
+        HIP_OK(hipEventRecord(S.ev_ccl, s_ccl));
+        HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_ccl, 0));
+        if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_acc, S.ev_out, 0));
+        if (!(skip & 4)) HIP_OK(dvc::launch_accumulate(a, h->s_acc));
+        HIP_OK(hipEventRecord(S.ev_acc, h->s_acc));
+        HIP_OK(hipStreamWaitEvent(h->s_out, S.ev_acc, 0));
+        if (timed && !fused) HIP_OK(hipEventRecord(h->ev[h->ev_used], h->s_out));
+        if (!(skip & 8)) HIP_OK(dvc::launch_out(a, h->s_out, fused));
+        if (timed && !fused) {
+            HIP_OK(hipEventRecord(h->ev[h->ev_used + 1], h->s_out));
+            h->ev_used += 2;
+        }
+        HIP_OK(hipEventRecord(S.ev_out, h->s_out));
+        h->prev_graph = false;
+        S.graph = false;
     }
-    HIP_OK(hipEventRecord(S.ev_out, h->s_out));
+    h->gcur ^= 1;
     S.recorded = true;
     h->seq++;
     h->frames += (uint64_t)n;
@@ -1023,6 +1252,13 @@ static int run_frames(dvc_fd* h, const uint8_t* bgr, size_t pitch, size_t fstrid
                                    overlay ? overlay + (size_t)f0 * ostride : nullptr,
                                    compressed ? compressed + (size_t)f0 * ostride : nullptr, ostride, h->crows);
             if (rc) return rc;
+        }
+        if (h->prev_graph && (acc_out || h->has_user)) {
+            // the last batch ran on its slot's graph stream: the acc copy and the
+            // caller's join below follow its accumulate and output stages
+            const Slot& L = h->slot[(h->seq + NSLOT - 1) % NSLOT];
+            HIP_OK(hipStreamWaitEvent(h->s_acc, L.ev_acc, 0));
+            HIP_OK(hipStreamWaitEvent(h->s_out, L.ev_out, 0));
         }
         if (acc_out) HIP_OK(hipMemcpy2DAsync(acc_out, W, h->acc, h->AP, W, H, hipMemcpyDeviceToDevice, h->s_acc));
         HIP_OK(join_user(h));
@@ -1174,6 +1410,14 @@ int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset)
     if (total_ms) *total_ms = t;
     if (launches) *launches = h->ev_used / 2;
     if (reset) h->ev_used = 0;
+    return DVC_OK;
+}
+
+int dvc_fd_graph_stats(const dvc_fd* h, uint64_t* batches, uint64_t* builds)
+{
+    if (!h) return fail(DVC_E_INVALID, "NULL handle");
+    if (batches) *batches = h->graph_batches;
+    if (builds) *builds = h->graph_builds;
     return DVC_OK;
 }
 

@@ -34,11 +34,15 @@
 
 #include "dvc_device.h"
 #include "fd_kernels.h"
+#include "klaunch.h"
 #include "dct_const.h"
 #include "yuv_px.h"
 #include "../../include/dvc.h"
+#include "tune.h"
 
 namespace dvc {
+
+thread_local std::vector<KNode>* g_krec = nullptr;   // klaunch.h
 
 // ------------------------------------------------------------ prime (fd:77) -
 // gray rows of gs = roundup(W, 4) bytes; the last quad of a row may be partial
@@ -2050,9 +2054,9 @@ hipError_t launch_prime(const uint8_t* bgr, int pitch, uint8_t* gray_tmp, uint32
                         int W, int H, int gs, const GaussTaps& k, hipStream_t s)
 {
     dim3 gq((gs / 4 + 255) / 256, H), gp((W + 255) / 256, H);
-    hipLaunchKernelGGL(k_gray, gq, dim3(256), 0, s, bgr, pitch, gray_tmp, W, H, gs);
-    hipLaunchKernelGGL(k_hblur_q8, gp, dim3(256), 0, s, gray_tmp, tmp32, W, H, gs, k);
-    hipLaunchKernelGGL(k_vblur_q8, gp, dim3(256), 0, s, tmp32, out, W, H, gs, k);
+    klaunch(k_gray, gq, dim3(256), 0, s, bgr, pitch, gray_tmp, W, H, gs);
+    klaunch(k_hblur_q8, gp, dim3(256), 0, s, gray_tmp, tmp32, W, H, gs, k);
+    klaunch(k_vblur_q8, gp, dim3(256), 0, s, tmp32, out, W, H, gs, k);
     return hipGetLastError();
 }
 
@@ -2067,9 +2071,9 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     // at least 8 frames per chunk — each extra chunk re-reads a warm-up frame
     // and adds waves competing with the contour filter (1080p x 191 at NW = 4:
     // 2 chunks, measured best of 1..9); DVC_FRONT_WAVES / DVC_FRONT_MIN override
-    static const int target = [] { const char* e = getenv("DVC_FRONT_WAVES"); return e ? std::max(1, atoi(e)) : 5120; }();
+    static const int target = [] { const char* e = dvc::tune_env("DVC_FRONT_WAVES"); return e ? std::max(1, atoi(e)) : 5120; }();
     int chunks = (target / NW + tx * ty / 2) / (tx * ty);
-    static const int minf = [] { const char* e = getenv("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
+    static const int minf = [] { const char* e = dvc::tune_env("DVC_FRONT_MIN"); return e ? std::max(1, atoi(e)) : 8; }();
     if (fo) {
         // fused outputs (4 workgroups per CU, 5 for 4:2:0 surfaces): chunks of ~48 frames
         // (1080p x 383: 8 chunks, 4352 workgroups; measured alone 373 k / 514 k /
@@ -2079,7 +2083,7 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
         // at least ~2048 workgroups (8 a CU) when the batch is short: 1080p x 32
         // frames as one chunk is 544 workgroups, half the device (4 chunks of 8
         // frames: 299.7 -> 314.4 k Mpx/s at --batch 32, experiments/README.md)
-        static const int fc = [] { const char* e = getenv("DVC_FUSED_CHUNKS"); return e ? atoi(e) : 0; }();
+        static const int fc = [] { const char* e = dvc::tune_env("DVC_FUSED_CHUNKS"); return e ? atoi(e) : 0; }();
         chunks = fc > 0 ? fc : std::max({1, n / 48, (2048 + tx * ty - 1) / (tx * ty)});
     }
     chunks = std::max(1, std::min(chunks, n / minf));
@@ -2088,11 +2092,11 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
     // XCD bands (k_front: each XCD walks a contiguous run of (chunk, tile row,
     // tile) ids): the fused front's default (+1.2 to +1.4 %, BGR and NV12),
     // not the plain one's; DVC_FRONT_XCD overrides
-    static const int xcd_env = [] { const char* e = getenv("DVC_FRONT_XCD"); return e ? atoi(e) : -1; }();
+    static const int xcd_env = [] { const char* e = dvc::tune_env("DVC_FRONT_XCD"); return e ? atoi(e) : -1; }();
     const int xcd = xcd_env >= 0 ? xcd_env : (fo ? 1 : 0);
     // frames in flight per workgroup: the fused BGR front 2 (+1 % against 1 at
     // 4 workgroups a CU, 119 VGPRs), the others 1; DVC_FRONT_PF overrides
-    static const int pf_env = [] { const char* e = getenv("DVC_FRONT_PF"); return e ? atoi(e) : 0; }();
+    static const int pf_env = [] { const char* e = dvc::tune_env("DVC_FRONT_PF"); return e ? atoi(e) : 0; }();
     const int pf = pf_env > 0 ? pf_env : (fo ? 2 : 1);
     const dim3 grid(tx, ty, chunks), block(64 * NW);
     const FrontOut none{};
@@ -2100,10 +2104,10 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
         if (fo) {
             // DVC_FRONT_LDS=<bytes> (experiment): unused dynamic LDS per workgroup, to
             // cap the fused front's workgroups per CU and leave room to the others
-            static const size_t pad = [] { const char* e = getenv("DVC_FRONT_LDS"); return e ? (size_t)atol(e) : 0; }();
+            static const size_t pad = [] { const char* e = dvc::tune_env("DVC_FRONT_LDS"); return e ? (size_t)atol(e) : 0; }();
             if constexpr (NW == 4) {
                 if (fo->B == 8) {   // 8x8 blocks (BGR frames; launch_front checked the rest)
-                    hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true, 8>), grid, block, pad, s, bgr, pitch, fstride, sf,
+                    klaunch((k_front<4, 1, DVC_FMT_BGR, true, 8>), grid, block, pad, s, bgr, pitch, fstride, sf,
                                        n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
                     return;
                 }
@@ -2111,50 +2115,50 @@ static void launch_front_nw(const uint8_t* bgr, int pitch, size_t fstride, const
             if constexpr (NW == 4) {
                 if (fo->i420) {   // I420 outputs (launch_front: B = 4, NW = 4)
                     if (sf.fmt == DVC_FMT_NV12)
-                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_NV12, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                        klaunch((k_front<4, 1, DVC_FMT_NV12, true, 4, true>), grid, block, pad, s, bgr, pitch,
                                            fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
                                            xcd, *fo);
                     else if (sf.fmt == DVC_FMT_I420)
-                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_I420, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                        klaunch((k_front<4, 1, DVC_FMT_I420, true, 4, true>), grid, block, pad, s, bgr, pitch,
                                            fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
                                            xcd, *fo);
                     else if (pf == 2)
-                        hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                        klaunch((k_front<4, 2, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
                                            fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
                                            xcd, *fo);
                     else
-                        hipLaunchKernelGGL((k_front<4, 1, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
+                        klaunch((k_front<4, 1, DVC_FMT_BGR, true, 4, true>), grid, block, pad, s, bgr, pitch,
                                            fstride, sf, n, chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh,
                                            xcd, *fo);
                     return;
                 }
             }
             if (sf.fmt == DVC_FMT_NV12)
-                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                klaunch((k_front<NW, 1, DVC_FMT_NV12, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             else if (sf.fmt == DVC_FMT_I420)
-                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                klaunch((k_front<NW, 1, DVC_FMT_I420, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             else if (pf == 2 && NW == 4)
-                hipLaunchKernelGGL((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                klaunch((k_front<4, 2, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             else
-                hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
+                klaunch((k_front<NW, 1, DVC_FMT_BGR, true>), grid, block, pad, s, bgr, pitch, fstride, sf, n,
                                    chunk, gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, *fo);
             return;
         }
     }
     if (sf.fmt == DVC_FMT_I420)
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_I420, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+        klaunch((k_front<NW, 1, DVC_FMT_I420, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else if (sf.fmt == DVC_FMT_NV12)
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_NV12, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+        klaunch((k_front<NW, 1, DVC_FMT_NV12, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else if (pf == 2)
-        hipLaunchKernelGGL((k_front<NW, 2, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+        klaunch((k_front<NW, 2, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
     else
-        hipLaunchKernelGGL((k_front<NW, 1, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
+        klaunch((k_front<NW, 1, DVC_FMT_BGR, false>), grid, block, 0, s, bgr, pitch, fstride, sf, n, chunk,
                            gray_in, gray_out, gs, mbits, g.W, g.H, g.WW, ithresh, xcd, none);
 }
 
@@ -2167,7 +2171,7 @@ hipError_t launch_front(const uint8_t* bgr, int pitch, size_t fstride, const Src
     if (fo && fo->B == 8 && sf.fmt != DVC_FMT_BGR) return hipErrorInvalidValue;   // 8x8: BGR frames only
     if (fo && fo->i420 && (fo->B != 4 || g.W % 4 || g.H % 4)) return hipErrorInvalidValue;   // I420: 4x4, whole blocks
     // waves per workgroup = tile height / 4 (DVC_FRONT_NW: 4, 8 or 16; the fused outputs need 4)
-    static const int nw = [] { const char* e = getenv("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
+    static const int nw = [] { const char* e = dvc::tune_env("DVC_FRONT_NW"); return e ? atoi(e) : 4; }();
     if (nw == 16 && !fo) launch_front_nw<16>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, nullptr);
     else if (nw == 8 && !(fo && (fo->B == 8 || fo->i420))) launch_front_nw<8>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
     else launch_front_nw<4>(bgr, pitch, fstride, sf, n, gray_in, gray_out, gs, mbits, g, ithresh, s, fo);
@@ -2211,7 +2215,7 @@ void resize_tables(int sw, int sh, int dw, int dh, int* host_x, int* host_y, int
 hipError_t launch_resize(const uint8_t* src, int spitch, size_t sstride, uint8_t* dst, int dpitch, size_t dstride,
                          int n, const ResizeTab& t, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_resize, dim3((t.dw + 255) / 256, t.dh, n), dim3(256), 0, s, src, spitch, sstride, dst, dpitch,
+    klaunch(k_resize, dim3((t.dw + 255) / 256, t.dh, n), dim3(256), 0, s, src, spitch, sstride, dst, dpitch,
                        dstride, t);
     return hipGetLastError();
 }
@@ -2241,7 +2245,7 @@ size_t ccl_max_lds(const RowGeom& g)
 // DVC_BAND_LDS_KB sizes it by total LDS instead (sweeps).
 static int band_budget(const RowGeom& g)
 {
-    static const int kb = [] { const char* e = getenv("DVC_BAND_LDS_KB"); return e ? std::max(8, atoi(e)) : 0; }();
+    static const int kb = [] { const char* e = dvc::tune_env("DVC_BAND_LDS_KB"); return e ? std::max(8, atoi(e)) : 0; }();
     const long long rest = kb * 1024LL - (long long)band_lds(g, BAND_ROWS, 0);
     return (int)std::max<long long>(1024, rest / 4);
 }
@@ -2251,7 +2255,7 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
     if (!c.rowb) return hipErrorInvalidValue;   // every kernel below finds its nodes through rowb
     // DVC_CCL_SUB=F (experiment): the five kernels over sub-batches of F frames
     static const int sub = [] {
-        const char* e = getenv("DVC_CCL_SUB");
+        const char* e = dvc::tune_env("DVC_CCL_SUB");
         return e ? atoi(e) : 0;
     }();
     if (sub > 0 && n > sub) {
@@ -2262,28 +2266,28 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
         return hipSuccess;
     }
     const int BH = band_rows(g), nb = (g.H + BH - 1) / BH, budget = band_budget(g);
-    hipLaunchKernelGGL(k_band, dim3(nb, n), dim3(BAND_NT), band_lds(g, BH, budget), s, c, g, budget);
+    klaunch(k_band, dim3(nb, n), dim3(BAND_NT), band_lds(g, BH, budget), s, c, g, budget);
     if (nb > 1)
-        hipLaunchKernelGGL(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
+        klaunch(k_merge, dim3((nb - 1 + 256 / MG - 1) / (256 / MG), n), dim3(256),
                            8 * merge_lds_words(g.WW) * (256 / MG), s, c, g, BH);
     // row groups of 8 lanes (8 rows a wave) for launches of >= ~100 k rows (96
     // frames at 1080p), 16 below (1080p x 383: +0.8 to +2.0 %, noisy +2.6 %,
     // x 128 +0.7 %, x 96 +0.7 %, 4K x 95 +0.1 to +0.4 %; 1080p x 64 -1 %, x 32
     // -4 %: the halved workgroup count no longer fills the device); DVC_CCL_CG overrides
-    static const int cg_env = [] { const char* e = getenv("DVC_CCL_CG"); return e ? atoi(e) : 0; }();
+    static const int cg_env = [] { const char* e = dvc::tune_env("DVC_CCL_CG"); return e ? atoi(e) : 0; }();
     const int cg = cg_env == 8 || cg_env == 16 ? cg_env : ((long long)n * g.H >= 96LL * 1080 ? 8 : 16);
     if (cg == 8) {
         const int grows = (g.H + cg_rows<8>() - 1) / cg_rows<8>();
         const size_t glds = (size_t)8 * g.WW * cg_rows<8>();
-        hipLaunchKernelGGL(k_resolve<8>, dim3(grows, n), dim3(256), glds, s, c, g);
-        hipLaunchKernelGGL(k_area<8>, dim3(grows, n), dim3(256), glds, s, c, g);
-        hipLaunchKernelGGL(k_paint<8>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
+        klaunch(k_resolve<8>, dim3(grows, n), dim3(256), glds, s, c, g);
+        klaunch(k_area<8>, dim3(grows, n), dim3(256), glds, s, c, g);
+        klaunch(k_paint<8>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
     } else {
         const int grows = (g.H + cg_rows<16>() - 1) / cg_rows<16>();
         const size_t glds = (size_t)8 * g.WW * cg_rows<16>();
-        hipLaunchKernelGGL(k_resolve<16>, dim3(grows, n), dim3(256), glds, s, c, g);
-        hipLaunchKernelGGL(k_area<16>, dim3(grows, n), dim3(256), glds, s, c, g);
-        hipLaunchKernelGGL(k_paint<16>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
+        klaunch(k_resolve<16>, dim3(grows, n), dim3(256), glds, s, c, g);
+        klaunch(k_area<16>, dim3(grows, n), dim3(256), glds, s, c, g);
+        klaunch(k_paint<16>, dim3(grows, n), dim3(256), glds, s, c, g, min_area2);
     }
     return hipGetLastError();
 }
@@ -2291,11 +2295,11 @@ hipError_t launch_ccl(const CclBufs& c, const RowGeom& g, int n, int64_t min_are
 template <int B>
 static hipError_t launch_acc(const BackArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_dilate<B>, dim3((a.g.WW * a.NBY + 255) / 256, a.n), dim3(256), 0, s, a);
+    klaunch(k_dilate<B>, dim3((a.g.WW * a.NBY + 255) / 256, a.n), dim3(256), 0, s, a);
     if (a.acc_fast)
-        hipLaunchKernelGGL((k_acc<B, true>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
+        klaunch((k_acc<B, true>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((k_acc<B, false>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
+        klaunch((k_acc<B, false>), dim3(a.SW, a.NBY), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -2303,8 +2307,8 @@ hipError_t launch_accumulate(const BackArgs& a, hipStream_t s)
 {
     if (a.B == 4) return launch_acc<4>(a, s);
     if (a.B == 8) return launch_acc<8>(a, s);
-    hipLaunchKernelGGL(k_dilate_rows, dim3((a.g.WW * a.g.H + 255) / 256, a.n), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_acc_rows, dim3(a.g.WW, a.g.H), dim3(64), 0, s, a);
+    klaunch(k_dilate_rows, dim3((a.g.WW * a.g.H + 255) / 256, a.n), dim3(256), 0, s, a);
+    klaunch(k_acc_rows, dim3(a.g.WW, a.g.H), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -2316,7 +2320,7 @@ static void launch_gen(const BackArgs& a, int rx0, int rx1, int ry0, int ry1, in
     R.njx = (rx1 - rx0 + R.jbx - 1) / R.jbx;
     const int njy = (ry1 - ry0 + R.jby - 1) / R.jby;
     const size_t lds = (size_t)8 * R.jbx * R.jby * a.B * a.B + (size_t)4 * R.jbx * R.jby;
-    hipLaunchKernelGGL(k_out_gen, dim3(R.njx * njy, a.n), dim3(256), lds, s, a, R, fast);
+    klaunch(k_out_gen, dim3(R.njx * njy, a.n), dim3(256), lds, s, a, R, fast);
 }
 
 hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
@@ -2339,7 +2343,7 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
     // 128 workgroups per CU (32768 on MI355X): measured best of 8k..64k beside
     // the CCL chain at 1080p x 191 (+1 % over 64/CU); DVC_OUT_WGS overrides
     static const int wgs = [] {
-        if (const char* e = getenv("DVC_OUT_WGS")) return std::max(1, atoi(e));
+        if (const char* e = dvc::tune_env("DVC_OUT_WGS")) return std::max(1, atoi(e));
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
         return 128 * cus;
@@ -2349,13 +2353,13 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
     const int f = a.sf.fmt;
     if (fix && B == 8) {   // the fused 8x8 front's fix-up: k_out's per-block pass, non-static blocks only
         if (a.out_i420 || a.obytes || f != DVC_FMT_BGR) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+        klaunch((k_out<8, DVC_FMT_BGR, true>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
         return hipGetLastError();
     }
     if (fix) {   // the fused front's speculative outputs (FrontOut: B = 4, BGR out in dword rows)
         if (B != 4 || a.obytes) return hipErrorInvalidValue;   // (I420 outputs: whole 4x4 blocks, create checked)
         static const int fwgs = [] {   // DVC_FIX_WGS: k_fix4 workgroups (default 6 per CU: all resident at 79 VGPRs)
-            if (const char* e = getenv("DVC_FIX_WGS")) return std::max(1, atoi(e));
+            if (const char* e = dvc::tune_env("DVC_FIX_WGS")) return std::max(1, atoi(e));
             int dev = 0, cus = 256;
             if (hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2363,22 +2367,27 @@ hipError_t launch_out(const BackArgs& a, hipStream_t s, bool fix)
             return 6 * cus;
         }();
         if (a.SW > 64) return hipErrorInvalidValue;   // rows of <= 64 words (W <= 16384 px): the scan's lanes
-        const int RG = std::max(1, 64 / a.SW), units = (a.NBY + RG - 1) / RG * a.n;
+        // block rows a unit (a wave): as many as the scan's 64 lanes take (8 at
+        // 1080p), fewer for short batches so that the launch still has ~1024
+        // waves (1080p x 1 frame: 270 one-row units instead of 34 eight-row
+        // ones — 27 -> ~5 us a call for the graph path's per-frame calls)
+        const int RG = std::max(1, std::min(64 / a.SW, a.NBY * a.n / 1024));
+        const int units = (a.NBY + RG - 1) / RG * a.n;
         const dim3 fg(std::max(1, std::min(fwgs, (units + 3) / 4)));
         const bool oi = a.out_i420;
-        if (a.sf.fmt == DVC_FMT_NV12 && oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_NV12, true>), fg, dim3(256), 0, s, a, RG);
-        else if (a.sf.fmt == DVC_FMT_NV12) hipLaunchKernelGGL((k_fix4<DVC_FMT_NV12, false>), fg, dim3(256), 0, s, a, RG);
-        else if (a.sf.fmt == DVC_FMT_I420 && oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_I420, true>), fg, dim3(256), 0, s, a, RG);
-        else if (a.sf.fmt == DVC_FMT_I420) hipLaunchKernelGGL((k_fix4<DVC_FMT_I420, false>), fg, dim3(256), 0, s, a, RG);
-        else if (oi) hipLaunchKernelGGL((k_fix4<DVC_FMT_BGR, true>), fg, dim3(256), 0, s, a, RG);
-        else hipLaunchKernelGGL((k_fix4<DVC_FMT_BGR, false>), fg, dim3(256), 0, s, a, RG);
+        if (a.sf.fmt == DVC_FMT_NV12 && oi) klaunch((k_fix4<DVC_FMT_NV12, true>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_NV12) klaunch((k_fix4<DVC_FMT_NV12, false>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_I420 && oi) klaunch((k_fix4<DVC_FMT_I420, true>), fg, dim3(256), 0, s, a, RG);
+        else if (a.sf.fmt == DVC_FMT_I420) klaunch((k_fix4<DVC_FMT_I420, false>), fg, dim3(256), 0, s, a, RG);
+        else if (oi) klaunch((k_fix4<DVC_FMT_BGR, true>), fg, dim3(256), 0, s, a, RG);
+        else klaunch((k_fix4<DVC_FMT_BGR, false>), fg, dim3(256), 0, s, a, RG);
     }
-    else if (B == 4 && f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (B == 4 && f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (B == 4) hipLaunchKernelGGL((k_out<4, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (f == DVC_FMT_I420) hipLaunchKernelGGL((k_out<8, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else if (f == DVC_FMT_NV12) hipLaunchKernelGGL((k_out<8, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
-    else hipLaunchKernelGGL((k_out<8, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4 && f == DVC_FMT_I420) klaunch((k_out<4, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4 && f == DVC_FMT_NV12) klaunch((k_out<4, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (B == 4) klaunch((k_out<4, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_I420) klaunch((k_out<8, DVC_FMT_I420, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else if (f == DVC_FMT_NV12) klaunch((k_out<8, DVC_FMT_NV12, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
+    else klaunch((k_out<8, DVC_FMT_BGR, false>), dim3(grid), dim3(256), 0, s, a, ntx, nty);
     return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@
 #include "host_common.h"
 #include "yuv_kernels.h"
 #include "of_kernels.h"
+#include "tune.h"
 
 using dvc_host::fail;
 
@@ -278,7 +279,7 @@ static bool of_direct(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fs
 // DVC_OF_YUV_DIRECT=0 forces the staged conversion (A/B).
 static bool of_direct_yuv(const dvc_of* h, const uint8_t* p, size_t pitch, size_t fstride, int n)
 {
-    static const int on = [] { const char* e = getenv("DVC_OF_YUV_DIRECT"); return e ? atoi(e) : 1; }();
+    static const int on = [] { const char* e = dvc::tune_env("DVC_OF_YUV_DIRECT"); return e ? atoi(e) : 1; }();
     return on && h->p.width % 4 == 0 && pitch % 4 == 0 && ((uintptr_t)p & 3) == 0 && (n <= 1 || fstride % 4 == 0);
 }
 
@@ -455,7 +456,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     h->s_pyr = h->stream;
     {
         // DVC_OF_PRIO=<flow><mask> (experiments): h / n / l stream priority each
-        const char* pe = getenv("DVC_OF_PRIO");
+        const char* pe = dvc::tune_env("DVC_OF_PRIO");
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         auto prio = [&](int i) {
@@ -515,7 +516,11 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
             return v >= 1 && v <= 64 ? v : dvc::FU_ROWS_LDS;
         }();
         h->lv[k].up_rows = 0;
-        for (int per = up_per; per >= 1 && !h->lv[k].up_rows; per = per > dvc::FU_ROWS ? dvc::FU_ROWS : 0) {
+        // DVC_OF_UP_GATHER (read per handle: tests compare the forms): the gather
+        // form k_flow_up on every level (up_rows = 0)
+        const bool gather = getenv("DVC_OF_UP_GATHER") != nullptr;
+        for (int per = gather ? 0 : up_per; per >= 1 && !h->lv[k].up_rows;
+             per = per > dvc::FU_ROWS ? dvc::FU_ROWS : 0) {
             int rows = 0;
             for (int y0 = 0; y0 < h->lv[k].h; y0 += per) {
                 const int ye = std::min(y0 + per, h->lv[k].h) - 1;
@@ -747,7 +752,7 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
     // iteration took ~3 ms beside it for 1.7 % of the pixels. Serial: +4 % (3
     // rounds, one box). DVC_OF_SERIAL=0 restores the overlap; =2 also holds
     // the flow of batch i until the mask stage of batch i-1 is done.
-    static const int serial = [] { const char* e = getenv("DVC_OF_SERIAL"); return e ? atoi(e) : 1; }();
+    static const int serial = [] { const char* e = dvc::tune_env("DVC_OF_SERIAL"); return e ? atoi(e) : 1; }();
     OfSlot& Sp = h->slot[(h->seq + 1) & 1];   // batch i-1
     // (experiments) =3: wait only for batch i-1's coarse levels, =4: for its
     // level 0's first iteration — the pyramid then fills the CUs the level-0

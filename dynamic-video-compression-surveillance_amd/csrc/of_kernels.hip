@@ -40,6 +40,7 @@
 #include "of_kernels.h"
 #include "dct_const.h"
 #include "yuv_px.h"
+#include "tune.h"
 
 namespace dvc {
 
@@ -2363,7 +2364,7 @@ size_t of_mask_min_lds(const OfGeom& g) { return of_band_lds(g, 1); }
 static int of_band_rows(const OfGeom& g, size_t* lds)
 {
     static const int bh0 = [] {   // DVC_OF_BH (experiments): rows per k_of_band workgroup, 8 / 4 / 2 / 1
-        const char* e = getenv("DVC_OF_BH");
+        const char* e = dvc::tune_env("DVC_OF_BH");
         const int v = e ? atoi(e) : 8;
         return v == 4 || v == 2 || v == 1 ? v : 8;
     }();
@@ -2530,7 +2531,7 @@ constexpr ScanCfg kScanCfg4[] = {{512, 12}, {512, 6}, {256, 6}, {384, 6}, {256, 
 int scan_cfg_index()
 {
     static const int v = [] {
-        const char* e = getenv("DVC_OF_SCAN");
+        const char* e = dvc::tune_env("DVC_OF_SCAN");
         const int k = e ? atoi(e) : 0;
         return k >= 0 && k < (int)(sizeof(kScanCfg4) / sizeof(kScanCfg4[0])) ? k : 0;
     }();
@@ -2603,7 +2604,7 @@ hipError_t of_launch_flow(const OfGeom& g, const Level* lv, const OfBufs& b, lon
                 if (A.src_mode == 1) {   // upsample into the level's other flow buffer (unused
                     // until iteration 1 writes it), then read it as a flow buffer
                     float* up = L.flow[1];
-                    if (L.up_rows > 0 && !getenv("DVC_OF_UP_GATHER"))
+                    if (L.up_rows > 0)   // the coarse rows fit in LDS (of_api.hip; 0 = the gather form)
                         hipLaunchKernelGGL(k_flow_up_lds, dim3(1, (L.h + L.up_per - 1) / L.up_per, n), dim3(256),
                                            (size_t)L.up_rows * A.sw * 8, s, A, up);
                     else

@@ -211,6 +211,12 @@ class FDWorker:
             N.check(k)
         return "k_front_fused" if k == N.KTIME_FRONT_FUSED else "k_out"
 
+    def graph_stats(self) -> dict:
+        """Batches launched as HIP graphs (the short-batch device path) and graphs built."""
+        b, g = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(self._lib.dvc_fd_graph_stats(self._h, ctypes.byref(b), ctypes.byref(g)))
+        return {"batches": int(b.value), "builds": int(g.value)}
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.dvc_fd_destroy(self._h)

@@ -37,6 +37,25 @@ def test_shipping_library_has_no_result_changing_knobs():
         assert knob not in blob, knob
 
 
+def test_shipping_library_reads_no_tuning_knobs():
+    """Launch-tuning knobs (grid sizes, chunks, priorities, LDS pads, A/B
+    switches) are read from the environment only by experiment builds
+    (csrc/tune.h): their names are absent from the shipping
+    library, whose only environment reads are the per-handle path selectors
+    and the fault injection the tests use."""
+    import re
+    import dvc_amd
+    blob = open(dvc_amd._native.build(), "rb").read()
+    names = set(re.findall(rb"DVC_[A-Z0-9_]{3,}", blob))
+    allowed = {b"DVC_FD_GRAPH", b"DVC_FD_FUSED8", b"DVC_OF_SCAN2", b"DVC_OF_UP_ROWS", b"DVC_OF_UP_GATHER",
+               b"DVC_OF_FAULT"}
+    for n in (b"DVC_PRIO", b"DVC_FRONT_WAVES", b"DVC_FUSED_CHUNKS", b"DVC_OUT_WGS", b"DVC_FIX_WGS", b"DVC_CCL_CG",
+              b"DVC_OF_SERIAL", b"DVC_OF_PRIO", b"DVC_OF_SCAN", b"DVC_OF_BH", b"DVC_FD_FUSED", b"DVC_ACC_GENERAL"):
+        assert n not in names, n
+    # (error texts name flags and formats: DVC_FLAG_*, DVC_FMT_*)
+    assert all(n in allowed or n.startswith((b"DVC_FLAG_", b"DVC_FMT_")) for n in names), names
+
+
 def test_abi_gaussian_taps_host_only():
     """dvc_gaussian_taps_q8 is pure host code: same taps as the oracle."""
     import dvc_amd

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Interleaved A/B of bench.py under environment variants (GPU box):
 #   tools/ab_env.sh <rounds> "<env A>" "<env B>" ... -- [bench args]
-# prints value per variant per round.
+# prints value per variant per round. Tuning knobs (csrc/tune.h) are read only
+# by an experiment build: tools/build_variant.sh build/libdvc_exp.so
+# -DDVC_EXPERIMENTS on the CPU side, then DVC_LIB_PATH=build/libdvc_exp.so here.
 R=$1; shift
 vars=()
 while [ "$1" != "--" ] && [ $# -gt 0 ]; do vars+=("$1"); shift; done
