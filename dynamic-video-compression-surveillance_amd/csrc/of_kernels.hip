@@ -96,39 +96,72 @@ __device__ __forceinline__ int ring(long long a, int n)
 // ------------------------------------------------- polynomial expansion -----
 // Steps C and D of FarnebackPolyExp (oc_poly_exp) for one tile whose smoothed
 // level image I is in LDS at rows [y0-PN, y0+PT_H-1+PN], cols [x0-PN, ...]
-// (in-image entries only). sv: PT_H x (PT_W+2PN) x 3 floats. INT: the tile and
-// its PN halo lie inside the image (no clamping; LDS offsets are constants).
-template <int PN, bool INT = false>
+// (in-image entries only), rows of SI floats. sv: PT_H x SV positions x 3
+// floats. INT: the tile and its PN halo lie inside the image (no clamping;
+// LDS offsets are constants). VEC (INT tiles, SI and SV multiples of 4): the
+// vertical part over groups of 4 columns as float4 vectors — the same float
+// operations per element in the same order (-ffp-contract=off), packed
+// (v_pk_mul_f32 / v_pk_add_f32) and read / written 16 B at a time.
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int PN, bool INT, int SI = PT_W + 2 * PN, int SV = PT_W + 2 * PN, bool VEC = false>
 __device__ __forceinline__ void poly_tile(const float* sI, float* sv, const PolyCoef& pc, int x0, int y0, int w,
                                           int h, float* __restrict__ R)
 {
     constexpr int IW = PT_W + 2 * PN;
+    static_assert(!VEC || (INT && SI % 4 == 0 && SV % 4 == 0 && SI >= IW + 3 - (IW + 3) % 4 && SV >= SI),
+                  "vector rows: 16-B aligned, whole groups of 4");
     const int tid = threadIdx.x;
-    // vertical part, float (oc_poly_exp: r = s*g0; t += g_k*(a+b) ...)
-    for (int idx = tid; idx < PT_H * IW; idx += 256) {
-        const int i = idx / IW, j = idx - i * IW;
-        const int y = y0 + i, x = x0 - PN + j;
-        if (!INT && (y >= h || x < 0 || x >= w)) continue;
-        const int li = i + PN;
-        float r0 = sI[li * IW + j] * pc.g[PN];
-        float r1 = 0.f, r2 = 0.f;
+    if constexpr (VEC) {
+        constexpr int NG = (IW + 3) / 4;   // column groups (the last one's extra columns are row padding)
+        // the taps as scalar values (readfirstlane: otherwise the compiler
+        // vectorises their kernel-argument loads through a private copy)
+        auto tap = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+        for (int it = tid; it < PT_H * NG; it += 256) {
+            const int i = it / NG, j = 4 * (it - i * NG), li = i + PN;
+            f4v r0 = *reinterpret_cast<const f4v*>(sI + li * SI + j) * tap(pc.g[PN]);
+            f4v r1 = 0.f, r2 = 0.f;
 #pragma unroll
-        for (int k = 1; k <= PN; ++k) {
-            const float g0 = pc.g[PN + k], g1 = pc.xg[PN + k], g2 = pc.xxg[PN + k];
-            const int ya = INT ? li - k : max(y - k, 0) - (y0 - PN), yb = INT ? li + k : min(y + k, h - 1) - (y0 - PN);
-            const float a = sI[ya * IW + j], b = sI[yb * IW + j];
-            const float p = a + b;
-            const float t0 = r0 + g0 * p;
-            const float t1 = r1 + g1 * (b - a);
-            const float t2 = r2 + g2 * p;
-            r0 = t0;
-            r1 = t1;
-            r2 = t2;
+            for (int k = 1; k <= PN; ++k) {
+                const float g0 = tap(pc.g[PN + k]), g1 = tap(pc.xg[PN + k]), g2 = tap(pc.xxg[PN + k]);
+                const f4v a = *reinterpret_cast<const f4v*>(sI + (li - k) * SI + j);
+                const f4v b = *reinterpret_cast<const f4v*>(sI + (li + k) * SI + j);
+                const f4v p = a + b;
+                r0 = r0 + g0 * p;
+                r1 = r1 + g1 * (b - a);
+                r2 = r2 + g2 * p;
+            }
+            f4v* v = reinterpret_cast<f4v*>(sv + (i * SV + j) * 3);   // positions j..j+3, 3 floats each
+            v[0] = f4v{r0.x, r1.x, r2.x, r0.y};
+            v[1] = f4v{r1.y, r2.y, r0.z, r1.z};
+            v[2] = f4v{r2.z, r0.w, r1.w, r2.w};
         }
-        float* v = sv + (i * IW + j) * 3;
-        v[0] = r0;
-        v[1] = r1;
-        v[2] = r2;
+    } else {
+        // vertical part, float (oc_poly_exp: r = s*g0; t += g_k*(a+b) ...)
+        for (int idx = tid; idx < PT_H * IW; idx += 256) {
+            const int i = idx / IW, j = idx - i * IW;
+            const int y = y0 + i, x = x0 - PN + j;
+            if (!INT && (y >= h || x < 0 || x >= w)) continue;
+            const int li = i + PN;
+            float r0 = sI[li * SI + j] * pc.g[PN];
+            float r1 = 0.f, r2 = 0.f;
+#pragma unroll
+            for (int k = 1; k <= PN; ++k) {
+                const float g0 = pc.g[PN + k], g1 = pc.xg[PN + k], g2 = pc.xxg[PN + k];
+                const int ya = INT ? li - k : max(y - k, 0) - (y0 - PN), yb = INT ? li + k : min(y + k, h - 1) - (y0 - PN);
+                const float a = sI[ya * SI + j], b = sI[yb * SI + j];
+                const float p = a + b;
+                const float t0 = r0 + g0 * p;
+                const float t1 = r1 + g1 * (b - a);
+                const float t2 = r2 + g2 * p;
+                r0 = t0;
+                r1 = t1;
+                r2 = t2;
+            }
+            float* v = sv + (i * SV + j) * 3;
+            v[0] = r0;
+            v[1] = r1;
+            v[2] = r2;
+        }
     }
     __syncthreads();
     // horizontal part (oc_poly_exp): float sub-expressions widened into double
@@ -137,14 +170,14 @@ __device__ __forceinline__ void poly_tile(const float* sI, float* sv, const Poly
         const int i = idx / PT_W, jx = idx - i * PT_W;
         const int y = y0 + i, x = x0 + jx;
         if (!INT && (y >= h || x >= w)) continue;
-        const float* c = sv + (i * IW + jx + PN) * 3;
+        const float* c = sv + (i * SV + jx + PN) * 3;
         const float gc = pc.g[PN];
         double b1 = (double)(c[0] * gc), b2 = 0, b3 = (double)(c[1] * gc), b4 = 0;
         double b5 = (double)(c[2] * gc), b6 = 0;
 #pragma unroll
         for (int k = 1; k <= PN; ++k) {
-            const float* P = INT ? c + 3 * k : sv + (i * IW + (min(x + k, w - 1) - (x0 - PN))) * 3;
-            const float* M = INT ? c - 3 * k : sv + (i * IW + (max(x - k, 0) - (x0 - PN))) * 3;
+            const float* P = INT ? c + 3 * k : sv + (i * SV + (min(x + k, w - 1) - (x0 - PN))) * 3;
+            const float* M = INT ? c - 3 * k : sv + (i * SV + (max(x - k, 0) - (x0 - PN))) * 3;
             const float gk = pc.g[PN + k], xgk = pc.xg[PN + k];
             const double tg = (double)(P[0] + M[0]);
 #if DVC_POLY_FMA
@@ -203,16 +236,27 @@ __device__ __forceinline__ uint32_t of_quad_gray(const uint8_t* f, int y, int px
     }
 }
 
+// LDS rows of the level-0 tile: the smoothed image and the vertical sums padded
+// to whole 16-B groups of 4 columns (IW = 74 -> 76 at poly_n 5), and the gray
+// kept as bytes, so that the blur and the vertical polynomial part run 4
+// columns a thread on float4 vectors (round 6: VERDICT r5 #3b)
+template <int PN> constexpr int f0_row() { return (PT_W + 2 * PN + 3) & ~3; }
+
 template <int PN, bool INT, int FMT>
 __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, uint8_t* __restrict__ gray_out,
                                             const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
-                                            const SrcFmt& sf, long long a0, float* sg, float* sI, float* sv)
+                                            const SrcFmt& sf, long long a0, float* sgv, float* sI)
 {
     // gray tile: rows y0-HG .., columns from x0-GX in whole 4-px quads (GX = 8 >= HG
     // keeps each quad's 12 BGR bytes 4-byte aligned: x0 % 64 == 0, pitch % 4 == 0)
     constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG, NQ = GW / 4;
-    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN, SR = f0_row<PN>();
     static_assert(HG <= GX, "halo wider than the quad pad");
+    static_assert(GX - PN - 1 >= 0, "the blur's left tap inside the gray row");
+    // LDS: gray bytes (GH x GW) and the horizontal blur (GH x SR floats) share
+    // sgv with the vertical sums written after the blur (poly_tile)
+    uint8_t* sgb = reinterpret_cast<uint8_t*>(sgv);
+    float* sh = sgv + (GH * GW + 15) / 16 * 4;
     const int tid = threadIdx.x, t = blockIdx.z;
     const int W = g.W, H = g.H;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
@@ -226,59 +270,92 @@ __device__ __forceinline__ void front0_tile(const OfGeom& g, const Level& lv, ui
         // padding (GP) and in LDS columns the clamped / reflected taps never read
         if (!INT && (y < 0 || y >= H || px < 0 || px >= W)) continue;
         const uint32_t gq = of_quad_gray<FMT>(f, y, px, pitch, sf);   // of:71 BGR2GRAY of 4 px
-        *reinterpret_cast<float4*>(sg + i * GW + 4 * q) =
-            make_float4((float)(gq & 255), (float)((gq >> 8) & 255), (float)((gq >> 16) & 255), (float)(gq >> 24));
+        *reinterpret_cast<uint32_t*>(sgb + i * GW + 4 * q) = gq;
         if (i >= HG && i < HG + PT_H && px >= x0 && px < x0 + PT_W)
             *reinterpret_cast<uint32_t*>(go + (size_t)y * g.GP + px) = gq;
     }
     __syncthreads();
-    // I = blur3(gray): horizontal pass at the 3 rows, then vertical (oc_blur_f32)
+    // I = blur3(gray) (oc_blur_f32): the horizontal pass of every gray row the
+    // vertical pass reads, then the vertical pass — the values the per-pixel
+    // form computed (acc = kc * c; acc += ks * (l + r), per row, then the same
+    // over the three rows), each horizontal sum once
     const float kc = lv.kf[1], ks = lv.kf[2];
-    for (int idx = tid; idx < IH * IW; idx += 256) {
-        const int i = idx / IW, j = idx - i * IW;
-        const int y = y0 - PN + i, x = x0 - PN + j;
-        if (!INT && (y < 0 || y >= H || x < 0 || x >= W)) continue;
-        const int xc = x - (x0 - GX);
-        const int xl = INT ? xc - 1 : reflect1(x - 1, W) - (x0 - GX), xr = INT ? xc + 1 : reflect1(x + 1, W) - (x0 - GX);
-        float hv[3];
-        const int ys[3] = {INT ? y - 1 : reflect1(y - 1, H), y, INT ? y + 1 : reflect1(y + 1, H)};
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const float* s = sg + (ys[q] - (y0 - HG)) * GW;
-            float acc = kc * s[xc];
-            acc += ks * (s[xl] + s[xr]);
-            hv[q] = acc;
+    if constexpr (INT) {
+        constexpr int NG = SR / 4;
+        for (int it = tid; it < GH * NG; it += 256) {   // row r = gray row y0 - HG + r, columns x0 - PN + 4 m ..
+            const int r = it / NG, m = it - r * NG;
+            // px x0 - PN + 4m - 1 .. + 4 are bytes O + 4m .. + 5 of the row, O = GX - PN - 1
+            // (2 at poly_n 5, 0 at 7): two aligned dwords hold them
+            constexpr int O = GX - PN - 1;
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(sgb + r * GW + 4 * m);
+            const uint32_t d0 = wp[0], d1 = wp[1];
+            auto px = [&](auto kc_) {
+                constexpr int bi = O + decltype(kc_)::value;
+                return (float)(((bi < 4 ? d0 : d1) >> (8 * (bi & 3))) & 255u);
+            };
+            using std::integral_constant;
+            const f4v lft = f4v{px(integral_constant<int, 0>{}), px(integral_constant<int, 1>{}),
+                                px(integral_constant<int, 2>{}), px(integral_constant<int, 3>{})};
+            const f4v ctr = f4v{lft.y, lft.z, lft.w, px(integral_constant<int, 4>{})};
+            const f4v rgt = f4v{lft.z, lft.w, ctr.w, px(integral_constant<int, 5>{})};
+            f4v acc = kc * ctr;
+            acc = acc + ks * (lft + rgt);
+            *reinterpret_cast<f4v*>(sh + r * SR + 4 * m) = acc;
         }
-        float acc = kc * hv[1];
-        acc += ks * (hv[0] + hv[2]);
-        sI[idx] = acc;
+        __syncthreads();
+        for (int it = tid; it < IH * NG; it += 256) {   // image row i = y0 - PN + i: gray rows i, i+1, i+2 (HG = PN + 1)
+            const int i = it / NG, m = it - i * NG;
+            const f4v h0 = *reinterpret_cast<const f4v*>(sh + i * SR + 4 * m);
+            const f4v h1 = *reinterpret_cast<const f4v*>(sh + (i + 1) * SR + 4 * m);
+            const f4v h2 = *reinterpret_cast<const f4v*>(sh + (i + 2) * SR + 4 * m);
+            f4v acc = kc * h1;
+            acc = acc + ks * (h0 + h2);
+            *reinterpret_cast<f4v*>(sI + i * SR + 4 * m) = acc;
+        }
+    } else {
+        for (int idx = tid; idx < GH * IW; idx += 256) {
+            const int r = idx / IW, j = idx - r * IW;
+            const int yg = y0 - HG + r, x = x0 - PN + j;
+            if (yg < 0 || yg >= H || x < 0 || x >= W) continue;
+            const uint8_t* s = sgb + r * GW - (x0 - GX);
+            float acc = kc * (float)s[x];
+            acc += ks * ((float)s[reflect1(x - 1, W)] + (float)s[reflect1(x + 1, W)]);
+            sh[r * SR + j] = acc;
+        }
+        __syncthreads();
+        for (int idx = tid; idx < IH * IW; idx += 256) {
+            const int i = idx / IW, j = idx - i * IW;
+            const int y = y0 - PN + i, x = x0 - PN + j;
+            if (y < 0 || y >= H || x < 0 || x >= W) continue;
+            const float* c = sh + j - (y0 - HG) * SR;
+            float acc = kc * c[y * SR];
+            acc += ks * (c[reflect1(y - 1, H) * SR] + c[reflect1(y + 1, H) * SR]);
+            sI[i * SR + j] = acc;
+        }
     }
     __syncthreads();
     float* R = lv.R + (size_t)ring(a0 + t, g.RS) * W * H * 5;
-    poly_tile<PN, INT>(sI, sv, g.pc, x0, y0, W, H, R);
+    poly_tile<PN, INT, SR, SR, INT>(sI, sgv, g.pc, x0, y0, W, H, R);
 }
 
 // Interior tiles (the tile with its GX-px quad pad and HG-row halo inside the
-// frame) take the unclamped form: the same arithmetic on the same values.
+// frame) take the unclamped, vectorised form: the same arithmetic on the same values.
 template <int PN, int FMT>
 __global__ void __launch_bounds__(256) k_of_front0(OfGeom g, Level lv, uint8_t* __restrict__ gray_out,
                                                    const uint8_t* __restrict__ bgr, int pitch, size_t fstride,
                                                    SrcFmt sf, long long a0)
 {
     constexpr int HG = PN + 1, GX = 8, GW = PT_W + 2 * GX, GH = PT_H + 2 * HG;
-    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
-    // sg (gray, read by the blur) and sv (the vertical sums, written after the
-    // blur's barrier) share one array: 22 KB instead of 31 KB a workgroup, six
-    // workgroups a CU instead of five (the 76-VGPR kernel allows six)
-    constexpr int SGV = GH * GW > PT_H * IW * 3 ? GH * GW : PT_H * IW * 3;
-    __shared__ __attribute__((aligned(16))) float sgv[SGV];
-    __shared__ float sI[IH * IW];
-    float* sg = sgv;
-    float* sv = sgv;
+    constexpr int IH = PT_H + 2 * PN, SR = f0_row<PN>();
+    // the gray bytes + the horizontal blur (read by the vertical blur) and the
+    // vertical sums (written after the blur's barrier) share one array
+    constexpr int A = (GH * GW + 15) / 16 * 4 + GH * SR, B = PT_H * SR * 3;
+    __shared__ __attribute__((aligned(16))) float sgv[A > B ? A : B];
+    __shared__ __attribute__((aligned(16))) float sI[IH * SR];
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     const bool interior = x0 >= GX && x0 + PT_W + GX <= g.W && y0 >= HG && y0 + PT_H + HG <= g.H;   // uniform
-    if (interior) front0_tile<PN, true, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sg, sI, sv);
-    else front0_tile<PN, false, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sg, sI, sv);
+    if (interior) front0_tile<PN, true, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sgv, sI);
+    else front0_tile<PN, false, FMT>(g, lv, gray_out, bgr, pitch, fstride, sf, a0, sgv, sI);
 }
 
 // ----------------------------------------------------------- level k > 0 ----
