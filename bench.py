@@ -377,6 +377,9 @@ def main():
         elapsed_runs.append(t1 - t0)
     # counters of the timed runs alone (every run steps the same frames): per run
     sts = [w.stats() for w in ws]
+    # FD: how the batches were launched — one HIP graph a batch (short batches of
+    # device frames, fd_api.hip enqueue_graph) or on the four stage streams
+    gstats = ws[0].graph_stats() if (not of and hasattr(ws[0]._lib, "dvc_fd_graph_stats")) else None
     st = {k: sum(x[k] - x0[k] for x, x0 in zip(sts, st0)) / runs for k in sts[0]}
     for w in ws:
         w.close()
@@ -473,6 +476,8 @@ def main():
                        "ring_frames": R, "noisy": args.noisy, "in_format": args.in_format,
                        "out_format": "mask + BGR" if of else args.out_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
+                       "launch_path": None if gstats is None else
+                       ("HIP graph a batch" if gstats["batches"] else "stage streams"),
                        "output_sets": max(1, args.out_ring),
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),

@@ -158,6 +158,11 @@ struct dvc_of {
     // batch i: s_pyr [wait flow(i-2)] pyramid(i); s_flow [wait pyramid(i),
     // mask(i-2)] flow(i); s_mask [wait flow(i)] vote/morphology/rects + out(i)
     hipStream_t s_pyr = nullptr, s_flow = nullptr, s_mask = nullptr;
+    // pyramid levels 2..L beside level 1 (of_launch_pyramid) on s_flow, idle
+    // while the batch's pyramid is built (its flow waits for it); the fork /
+    // join events. (A fifth stream would share one of the 4 hardware queues
+    // with another stage and serialise it: measured, experiments/README.md.)
+    hipEvent_t ev_gray = nullptr, ev_side = nullptr;
     OfSlot slot[2];
     uint64_t seq = 0;
     dvc::OfGeom g{};
@@ -196,7 +201,7 @@ static void of_free(dvc_of* h)
     for (OfSlot& sl : h->slot)
         for (hipEvent_t e : {sl.ev_pyr, sl.ev_flow, sl.ev_mask, sl.ev_l1, sl.ev_l0a})
             if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->ev_user, h->ev_join})
+    for (hipEvent_t e : {h->ev_user, h->ev_join, h->ev_gray, h->ev_side})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {h->s_flow, h->s_mask, h->stream})
         if (st) (void)hipStreamDestroy(st);
@@ -451,7 +456,7 @@ int dvc_of_create(const dvc_of_params* prm, int device, void* hip_stream, dvc_of
     // chain (interleaved sweep after the packed M phase: equal 16.15 k, flow +
     // mask high / pyramid low 15.88 k Mpx/s)
     if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-    for (hipEvent_t* ev : {&h->ev_user, &h->ev_join})
+    for (hipEvent_t* ev : {&h->ev_user, &h->ev_join, &h->ev_gray, &h->ev_side})
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     h->s_pyr = h->stream;
     {
@@ -771,7 +776,8 @@ static int of_enqueue(dvc_of* h, const uint8_t* d, int dp, size_t fstride, int n
         dp = kp;
         fstride = kfs;
     }
-    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, sf, a0, n, h->s_pyr));
+    HIP_OK(dvc::of_launch_pyramid(h->g, h->lv, h->b, d, dp, fstride, sf, a0, n, h->s_pyr, h->s_flow, h->ev_gray,
+                                  h->ev_side));
     HIP_OK(hipEventRecord(S.ev_pyr, h->s_pyr));
     HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_pyr, 0));
     if (S.recorded) HIP_OK(hipStreamWaitEvent(h->s_flow, S.ev_mask, 0));

@@ -132,8 +132,10 @@ struct OfOutArgs {
 // 4:2:0 decoder surfaces read in place (luma rows of `pitch`, chroma at
 // sf.uoff / sf.voff, rows of sf.cpitch; fd_kernels.h SrcFmt), converted as
 // cvtColor YUV2BGR per pixel as they load (what cap.read() returns, of:66)
+// s2 / ev_gray / ev_side (all or none): levels 2..L on s2 beside level 1 on s
 hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
-                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s);
+                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s,
+                             hipStream_t s2 = nullptr, hipEvent_t ev_gray = nullptr, hipEvent_t ev_side = nullptr);
 // Farneback levels k_hi down to k_lo (L..0 in total, coarse to fine) for frames
 // a0..a0+n-1 (prev = a-1); level 0's last iteration -> raw motion bits in mring
 // `kernel` (nullable): which flow kernel the launches of level k_lo took —

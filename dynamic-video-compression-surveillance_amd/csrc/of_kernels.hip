@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(256) k_pyr_v(OfGeom g, Level lv)
 template <int PN, bool INT>
 __device__ __forceinline__ void pyr_poly_tile(const OfGeom& g, const Level& lv, long long a0, float* sI, float* sv)
 {
-    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
+    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN, SR = f0_row<PN>();
     const int tid = threadIdx.x, t = blockIdx.z;
     const int w = lv.w, h = lv.h, n2 = 2 * w;
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
@@ -502,19 +502,19 @@ __device__ __forceinline__ void pyr_poly_tile(const OfGeom& g, const Level& lv, 
         const float* v1 = v0 + n2;
         const float t0 = v0[0] * tx.w0 + v0[1] * tx.w1;
         const float t1 = v1[0] * tx.w0 + v1[1] * tx.w1;
-        sI[idx] = t0 * ty.w0 + t1 * ty.w1;
+        sI[i * SR + j] = t0 * ty.w0 + t1 * ty.w1;
     }
     __syncthreads();
     float* R = lv.R + (size_t)ring(a0 + t, g.RS) * w * h * 5;
-    poly_tile<PN, INT>(sI, sv, g.pc, x0, y0, w, h, R);
+    poly_tile<PN, INT, SR, SR, INT>(sI, sv, g.pc, x0, y0, w, h, R);   // rows padded to 16 B: the vector form
 }
 
 template <int PN>
 __global__ void __launch_bounds__(256) k_pyr_poly(OfGeom g, Level lv, long long a0)
 {
-    constexpr int IW = PT_W + 2 * PN, IH = PT_H + 2 * PN;
-    __shared__ float sI[IH * IW];
-    __shared__ float sv[PT_H * IW * 3];
+    constexpr int IH = PT_H + 2 * PN, SR = f0_row<PN>();
+    __shared__ __attribute__((aligned(16))) float sI[IH * SR];
+    __shared__ __attribute__((aligned(16))) float sv[PT_H * SR * 3];
     const int x0 = blockIdx.x * PT_W, y0 = blockIdx.y * PT_H;
     if (x0 >= PN && x0 + PT_W + PN <= lv.w && y0 >= PN && y0 + PT_H + PN <= lv.h)
         pyr_poly_tile<PN, true>(g, lv, a0, sI, sv);
@@ -2468,7 +2468,8 @@ static long long reduce_frame(const OfGeom& g, long long a0)
 }
 
 hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, const uint8_t* bgr, int pitch,
-                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s)
+                             size_t fstride, const SrcFmt& sf, long long a0, int n, hipStream_t s, hipStream_t s2,
+                             hipEvent_t ev_gray, hipEvent_t ev_side)
 {
     a0 = reduce_frame(g, a0);
     if (n <= 0) return hipSuccess;
@@ -2484,18 +2485,34 @@ hipError_t of_launch_pyramid(const OfGeom& g, const Level* lv, const OfBufs& b, 
         }
 #undef DVC_FRONT0
     }
+    // Levels 1..L each smooth and resize the full-resolution gray (OpenCV's
+    // pyramid, not a recursive one), so they are independent: with a side
+    // stream, levels 2..L run beside level 1 (their latency-bound blur passes
+    // overlap), and s waits for them at the end
+    const bool side = s2 && ev_gray && ev_side && g.L >= 2;
+    if (side) {
+        hipError_t e = hipEventRecord(ev_gray, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s2, ev_gray, 0);
+        if (e != hipSuccess) return e;
+    }
     for (int k = 1; k <= g.L; ++k) {
+        hipStream_t sk = side && k >= 2 ? s2 : s;
         if ((size_t)8 * g.GP <= PH_F32_LDS)
-            hipLaunchKernelGGL(k_pyr_h<true>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)8 * g.GP, s, g,
+            hipLaunchKernelGGL(k_pyr_h<true>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)8 * g.GP, sk, g,
                                lv[k], b.gray);
         else   // wide frames: byte rows (GP <= 65520 B of LDS)
-            hipLaunchKernelGGL(k_pyr_h<false>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)g.GP, s, g,
+            hipLaunchKernelGGL(k_pyr_h<false>, dim3((g.H + PH_ROWS - 1) / PH_ROWS, n), dim3(256), (size_t)g.GP, sk, g,
                                lv[k], b.gray);
         hipLaunchKernelGGL(k_pyr_v, dim3((2 * lv[k].w + 255) / 256, (2 * lv[k].h + PV_ROWS - 1) / PV_ROWS, n), dim3(256),
-                           0, s, g, lv[k]);
+                           0, sk, g, lv[k]);
         dim3 gp((lv[k].w + PT_W - 1) / PT_W, (lv[k].h + PT_H - 1) / PT_H, n);
-        if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, s, g, lv[k], a0);
-        else hipLaunchKernelGGL(k_pyr_poly<7>, gp, dim3(256), 0, s, g, lv[k], a0);
+        if (g.pc.n == 5) hipLaunchKernelGGL(k_pyr_poly<5>, gp, dim3(256), 0, sk, g, lv[k], a0);
+        else hipLaunchKernelGGL(k_pyr_poly<7>, gp, dim3(256), 0, sk, g, lv[k], a0);
+    }
+    if (side) {
+        hipError_t e = hipEventRecord(ev_side, s2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_side, 0);
+        if (e != hipSuccess) return e;
     }
     return hipGetLastError();
 }
