@@ -162,3 +162,33 @@ def test_of_bench_config(gpu_lib, oracle_lib):
     wf.close()
     ref.close()
     assert checked >= 5
+
+
+def test_fd_headline_launch_every_frame_vs_oracle(gpu_lib, oracle_lib):
+    """The headline launch itself, every frame: one 383-frame dvc_fd_step_batch
+    of bench.py's 1080p sequence (configs[1], device frames, the stage-stream
+    pipeline) against a sequential oracle replay of the same 383 frames —
+    overlay and compressed frame bit for bit at every frame, and the stats.
+    (~45 s of oracle time on one core; the strided transition checks above
+    cover the second pass and the other configurations.)"""
+    import torch
+    dev = torch.device("cuda", 0)
+    W, H, batch = 1920, 1080, 383
+    ring, idx, seq, first = _sequence(W, H, batch + 1, False, seed=0, dev=dev)
+    ov = torch.empty((batch, H, W, 3), dtype=torch.uint8, device=dev)
+    cp = torch.empty_like(ov)
+    w = gpu_lib.FDWorker(W, H, device_ptrs=True, max_batch=batch)
+    w.prime(first)
+    w.step_batch(seq[:batch], ov, cp)
+    w.sync()
+    st = w.stats()
+    assert w.graph_stats()["batches"] == 0       # the stage-stream path (the graph path is for <= 32 frames)
+    w.close()
+    ref = oracle_lib.OracleFD(W, H)
+    ref.prime(ring[0])
+    for t in range(batch):
+        rov, rcp, _ = ref.step(ring[idx[t]])
+        assert np.array_equal(ov[t].cpu().numpy(), rov), f"overlay != oracle at frame {t}"
+        assert np.array_equal(cp[t].cpu().numpy(), rcp), f"compressed != oracle at frame {t}"
+    assert st == ref.stats()
+    ref.close()
