@@ -938,8 +938,19 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
             (void)hipGraphDestroy(S.graphs[lru].g);
             S.graphs.erase(S.graphs.begin() + (long)lru);
         }
-        S.graphs.emplace_back();
-        G = &S.graphs.back();
+        FdGraph NG;
+        // a failed build leaves nothing behind: the graph is kept only once instantiated
+        struct Drop {
+            FdGraph& x;
+            bool keep = false;
+            ~Drop()
+            {
+                if (keep) return;
+                if (x.ge) (void)hipGraphExecDestroy(x.ge);
+                if (x.g) (void)hipGraphDestroy(x.g);
+            }
+        } drop{NG};
+        G = &NG;
         HIP_OK(hipGraphCreate(&G->g, 0));
         // (no wait for the previous batch's contour filter: the slot has its own
         // working set; no record of this one's: Slot::graph — an event node costs
@@ -973,6 +984,9 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
             G->rec[sg].swap(rec[sg]);
         }
         HIP_OK(hipGraphInstantiate(&G->ge, G->g, nullptr, nullptr, 0));
+        drop.keep = true;
+        S.graphs.push_back(std::move(NG));
+        G = &S.graphs.back();
         h->graph_builds++;
     }
     if (S.recorded) HIP_OK(hipStreamWaitEvent(z, S.ev_out, 0));
