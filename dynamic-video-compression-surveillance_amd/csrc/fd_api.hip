@@ -132,8 +132,11 @@ struct FdGraph {
     uint64_t used = 0;                       // seq of its last launch (least recently used is replaced)
 };
 constexpr int NGRAPH = 4;                    // graphs kept per slot (launch shapes: frame count, outputs, format)
-constexpr int GRAPH_MAX_FRAMES = 32;         // batches up to this many frames take the graph path (the
-                                             // drop-in's read-ahead; each slot's own filter set holds as many)
+#ifndef DVC_GRAPH_MAX_FRAMES
+#define DVC_GRAPH_MAX_FRAMES 32
+#endif
+constexpr int GRAPH_MAX_FRAMES = DVC_GRAPH_MAX_FRAMES;   // batches up to this many frames take the graph path
+                                             // (the drop-in's read-ahead; each slot's own filter set holds as many)
 
 // Buffers of one batch in flight (max_batch frames): motion masks, contour-
 // filter scratch, kept masks, the dilate -> accumulate -> out bits, and the
@@ -961,11 +964,17 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
         auto dep = [&]() { return last ? 1u : 0u; };
         for (int sg = 0; sg < 4; ++sg) {
             hipGraphNode_t nd = nullptr;
-            if (waits[sg]) {
-                HIP_OK(hipGraphAddEventWaitNode(&nd, G->g, last ? &last : nullptr, dep(), waits[sg]));
-                last = nd;
-            }
-            for (dvc::KNode& kn : rec[sg]) {
+            // the accumulate stage waits for the previous batch's accumulate only
+            // before its last kernel (k_acc: the accumulated mask); k_dilate reads
+            // this batch's kept mask alone
+            const size_t wat = sg == 2 && !rec[sg].empty() ? rec[sg].size() - 1 : 0;
+            for (size_t u = 0; u <= rec[sg].size(); ++u) {
+                if (u == wat && waits[sg]) {
+                    HIP_OK(hipGraphAddEventWaitNode(&nd, G->g, last ? &last : nullptr, dep(), waits[sg]));
+                    last = nd;
+                }
+                if (u == rec[sg].size()) break;
+                dvc::KNode& kn = rec[sg][u];
                 hipKernelNodeParams kp{};
                 kp.func = const_cast<void*>(kn.f);
                 kp.gridDim = kn.grid;

@@ -40,6 +40,7 @@ if [ "$PART" = a ]; then
   b fd_noisy --noisy
   b fd_nv12_input --in-format NV12
 else
+  b fd_1080p_box_b
   b fd_per_frame --per-frame --runs 3 --steps 10 --warmup 2
   b fd_batch8 --batch 8 --runs 3
   b fd_batch32 --batch 32 --runs 3
