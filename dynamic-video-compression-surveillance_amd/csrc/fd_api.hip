@@ -130,13 +130,19 @@ struct FdGraph {
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     uint64_t used = 0;                       // seq of its last launch (least recently used is replaced)
+    bool shared = false;                     // its contour filter runs on the shared working set:
+    hipGraphNode_t wait_ccl = nullptr;       //   the wait for the set's previous user (event set per launch)
+    hipEvent_t wait_ev = nullptr;            //   the event that node waits for now
 };
 constexpr int NGRAPH = 4;                    // graphs kept per slot (launch shapes: frame count, outputs, format)
-#ifndef DVC_GRAPH_MAX_FRAMES
-#define DVC_GRAPH_MAX_FRAMES 32
+#ifndef DVC_GRAPH_OWN_CCL_FRAMES
+#define DVC_GRAPH_OWN_CCL_FRAMES 128
 #endif
-constexpr int GRAPH_MAX_FRAMES = DVC_GRAPH_MAX_FRAMES;   // batches up to this many frames take the graph path
-                                             // (the drop-in's read-ahead; each slot's own filter set holds as many)
+// graph batches up to this many frames run their contour filter on the slot's
+// own working set (Slot::gc: consecutive batches' filters overlap; four sets of
+// up to 128 1080p frames are ~9 GB); longer ones on the shared set the stage
+// streams use, after its previous user's filter
+constexpr int GRAPH_OWN_CCL_FRAMES = DVC_GRAPH_OWN_CCL_FRAMES;
 
 // Buffers of one batch in flight (max_batch frames): motion masks, contour-
 // filter scratch, kept masks, the dilate -> accumulate -> out bits, and the
@@ -154,14 +160,16 @@ struct Slot {
     // when not requested): a fused front writes outputs before the previous
     // batches' k_fix4 have run, so it waits for those that write the same bytes
     uintptr_t olo[2] = {0, 0}, ohi[2] = {0, 0};
-    bool graph = false;     // its last batch ran as a graph: only ev_front, ev_acc, ev_out were recorded
+    bool graph = false;     // its last batch ran as a graph: ev_front, ev_acc, ev_out were recorded,
+    bool shared_ccl = false;  // and ev_ccl when its contour filter ran on the shared working set
     std::vector<FdGraph> graphs;   // the graph path's graphs of this slot's batches
     // the graph path's contour filter: the slot's own working set (S.c's
     // mbits / kbits / kocc with its own run index, parents, areas, filled
     // bits), so consecutive batches' filters overlap instead of queueing on
-    // one shared set; allocated at the slot's first graph batch
+    // one shared set; grown at the slot's graph batches (graph_ccl)
     dvc::CclBufs gc{};
     std::vector<void*> gc_mem;
+    int gc_frames = 0;      // frames gc holds
 };
 
 // Batches in flight: four slots (the graph path launches each slot's batches
@@ -271,6 +279,7 @@ static void free_all(dvc_fd* h)
         s.graphs.clear();
         for (void* p : s.gc_mem) (void)hipFree(p);
         s.gc_mem.clear();
+        s.gc_frames = 0;
     }
     for (Stage& s : h->stage) {
         for (void* p : {(void*)s.d_in, (void*)s.d_ov, (void*)s.d_cp})
@@ -852,27 +861,40 @@ int dvc_fd_set_state(dvc_fd* h, const uint8_t* prev_gray, const uint8_t* acc)
 
 }  // extern "C"
 
-// The graph path of one batch (device frames read in place, <= GRAPH_MAX_FRAMES
-// frames, no KTIMING): the four stages' launches are recorded (dvc::klaunch),
+// The graph path of one batch (device frames read in place, no KTIMING): the
+// four stages' launches are recorded (dvc::klaunch),
 // matched against this slot's graphs by launch shape and launched as one
 // graph on the slot's graph stream. A call then costs one graph launch and a
 // few argument updates instead of nine launches and eleven event operations
 // across four streams (~80 us of host time a call, profiles/r6_fd_per_call_*).
-// Chain: [wait P.front] front [rec S.front] contour filter [rec S.ccl]
-// [wait P.acc] dilate, accumulate [rec S.acc] outputs [rec S.out], P = the
-// previous batch's slot — the recurrences the stage streams give the direct
-// path (previous gray, accumulated mask); the contour filter runs on the
-// slot's own working set (graph_ccl), so it needs no order across batches. Before the launch, on the graph stream: the slot's
+// Chain: [wait P.front] front [rec S.front] contour filter, dilate [wait P.acc]
+// accumulate [rec S.acc] outputs [rec S.out], P = the previous batch's slot —
+// the recurrences the stage streams give the direct path (previous gray,
+// accumulated mask). A short batch's contour filter runs on the slot's own
+// working set (graph_ccl) and needs no order across batches; a longer one's on
+// the shared set, between [wait for the set's previous user] and [rec S.ccl].
+// Before the launch, on the graph stream: the slot's
 // previous batch (S.out: every buffer of the slot is free) and `wait_out`
 // (earlier batches whose outputs the fused front overwrites).
-// The slot's own contour-filter working set for graph batches (Slot::gc), for
-// min(max_batch, GRAPH_MAX_FRAMES) frames: ~17 MB a 1080p frame.
-static int graph_ccl(dvc_fd* h, Slot& S)
+// The slot's own contour-filter working set for short graph batches (Slot::gc):
+// ~17 MB a 1080p frame, grown to the batch (powers of two up to
+// min(max_batch, GRAPH_OWN_CCL_FRAMES) frames), so per-frame calls hold four
+// one-frame sets. A graph keeps the old pointers until its next launch sets
+// the changed arguments.
+static int graph_ccl(dvc_fd* h, Slot& S, int n)
 {
-    if (!S.gc_mem.empty()) return DVC_OK;
-    const int gmb = std::min(h->max_batch, GRAPH_MAX_FRAMES);
+    if (n <= S.gc_frames) return DVC_OK;
+    int cap = 1;
+    while (cap < n) cap *= 2;
+    cap = std::min(cap, std::min(h->max_batch, GRAPH_OWN_CCL_FRAMES));
+    if (!S.gc_mem.empty()) {
+        if (S.recorded) HIP_OK(hipEventSynchronize(S.ev_out));   // the slot's last batch is done with the set
+        for (void* q : S.gc_mem) (void)hipFree(q);
+        S.gc_mem.clear();
+        S.gc_frames = 0;
+    }
     size_t sz[dvc::CclBufs::NARR];
-    dvc::CclBufs::sizes(h->g, gmb, sz);
+    dvc::CclBufs::sizes(h->g, cap, sz);
     S.gc = S.c;
     void** ptrs[dvc::CclBufs::NARR];
     S.gc.ptrs(ptrs);
@@ -891,17 +913,23 @@ static int graph_ccl(dvc_fd* h, Slot& S)
     }
     // every frame slice's OUTSIDE gap node is its own root before any k_band (as at create)
     HIP_OK(hipMemsetAsync(S.gc.gpar, 0, sz[6], graph_stream(h, (int)(&S - h->slot))));
+    S.gc_frames = cap;
     return DVC_OK;
 }
 
-static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], const std::vector<hipEvent_t>& wait_out)
+static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], const std::vector<hipEvent_t>& wait_out,
+                         bool shared)
 {
     const int k = (int)(h->seq % NSLOT);
     Slot& P = h->slot[(h->seq + NSLOT - 1) % NSLOT];
     hipStream_t z = graph_stream(h, k);
+    // the shared working set's previous user is done with it: the previous
+    // batch's filter when it ran there (ev_ccl), else its accumulate (ev_acc,
+    // which follows every earlier batch's accumulate, each after its filter)
+    const hipEvent_t ccl_ev = P.recorded && P.graph && !P.shared_ccl ? P.ev_acc : P.ev_ccl;
     FdGraph* G = nullptr;
     for (FdGraph& x : S.graphs) {
-        bool same = true;
+        bool same = x.shared == shared;
         for (int sg = 0; sg < 4 && same; ++sg) {
             same = x.rec[sg].size() == rec[sg].size();
             for (size_t u = 0; same && u < rec[sg].size(); ++u) same = x.rec[sg][u].same_shape(rec[sg][u]);
@@ -931,6 +959,10 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
                 kp.kernelParams = pp.data();
                 HIP_OK(hipGraphExecKernelNodeSetParams(G->ge, G->node[sg][u], &kp));
             }
+        if (shared && G->wait_ev != ccl_ev) {
+            HIP_OK(hipGraphExecEventWaitNodeSetEvent(G->ge, G->wait_ccl, ccl_ev));
+            G->wait_ev = ccl_ev;
+        }
     } else {
         if ((int)S.graphs.size() >= NGRAPH) {   // replace the least recently used one
             size_t lru = 0;
@@ -955,11 +987,12 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
         } drop{NG};
         G = &NG;
         HIP_OK(hipGraphCreate(&G->g, 0));
-        // (no wait for the previous batch's contour filter: the slot has its own
-        // working set; no record of this one's: Slot::graph — an event node costs
-        // ~5 us of the chain's latency on the device)
-        const hipEvent_t waits[4] = {P.ev_front, nullptr, P.ev_acc, nullptr};
-        const hipEvent_t recs[4] = {S.ev_front, nullptr, S.ev_acc, S.ev_out};
+        // (short batches: no wait for the previous batch's contour filter, the
+        // slot has its own working set, and no record of this one's — an event
+        // node costs ~5 us of the chain's latency on the device)
+        G->shared = shared;
+        const hipEvent_t waits[4] = {P.ev_front, shared ? ccl_ev : nullptr, P.ev_acc, nullptr};
+        const hipEvent_t recs[4] = {S.ev_front, shared ? S.ev_ccl : nullptr, S.ev_acc, S.ev_out};
         hipGraphNode_t last = nullptr;   // one chain: every node depends on the one before
         auto dep = [&]() { return last ? 1u : 0u; };
         for (int sg = 0; sg < 4; ++sg) {
@@ -971,6 +1004,10 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
             for (size_t u = 0; u <= rec[sg].size(); ++u) {
                 if (u == wat && waits[sg]) {
                     HIP_OK(hipGraphAddEventWaitNode(&nd, G->g, last ? &last : nullptr, dep(), waits[sg]));
+                    if (sg == 1) {
+                        G->wait_ccl = nd;
+                        G->wait_ev = waits[sg];
+                    }
                     last = nd;
                 }
                 if (u == rec[sg].size()) break;
@@ -1006,18 +1043,18 @@ static int enqueue_graph(dvc_fd* h, Slot& S, std::vector<dvc::KNode> (&rec)[4], 
     return DVC_OK;
 }
 
-// Enqueue one batch i of n <= max_batch frames, slot S = i % 3 (j = i - 3 =
-// the slot's previous batch):
+// Enqueue one batch i of n <= max_batch frames, slot S = i % NSLOT (j = i - NSLOT
+// = the slot's previous batch):
 //   s_front:         [wait ccl(j) (+ out(j) when staging or fused; fused: also
-//                    out(i-1), out(i-2) where their output bytes overlap)]
+//                    out(i-1) .. out(j+1) where their output bytes overlap)]
 //                    stage, front(i) (fused: + speculative outputs) -> ev_front   (S.mbits free)
 //   stream:          [wait ev_front, acc(j)]  contour filter(i) -> ev_ccl (S.kbits free)
 //   s_acc:           [wait ev_ccl, out(j)]    dilate + accumulate(i) -> ev_acc (S bits free)
 //   s_out:           [wait ev_acc]            k_out(i), or k_out_gen + k_fix4(i) when fused -> ev_out
 // so front(i+2), the contour filter of i+1, the accumulation of i and the
 // output of i-1 can all be in flight; the two recurrences (previous gray,
-// accumulated mask) are serial, each on its own stream. Short batches of
-// device frames take the graph path instead (enqueue_graph): the same
+// accumulated mask) are serial, each on its own stream. Batches of device
+// frames read in place take the graph path instead (enqueue_graph): the same
 // kernels, arguments and dependencies.
 static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fstride, int n, uint8_t* ov, uint8_t* cp,
                          size_t ostride, int crows)
@@ -1040,16 +1077,17 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
 #endif
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
     // the graph path: device frames the kernels read in place (no staging
-    // launches), short batches; DVC_FD_GRAPH=0 at create turns it off
+    // launches); DVC_FD_GRAPH=0 at create turns it off
     const bool graph = h->graph_ok && (h->p.flags & DVC_FLAG_DEVICE_PTRS) && !timed && !skip &&
-                       n <= GRAPH_MAX_FRAMES &&
                        (direct_frames(h, src, pitch, fstride, n) || direct_yuv(h, src, pitch, fstride, n));
     if (!graph && h->prev_graph) {
         // the previous batch ran on its slot's graph stream: the stage streams
         // take its recurrences from its events
         const Slot& P = h->slot[(h->seq + NSLOT - 1) % NSLOT];
         HIP_OK(hipStreamWaitEvent(h->s_front, P.ev_front, 0));
-        HIP_OK(hipStreamWaitEvent(s_ccl, P.ev_out, 0));   // (a graph batch records no ev_ccl)
+        // (a short graph batch records no ev_ccl: its ev_acc follows every
+        // earlier batch's filter on the shared working set)
+        HIP_OK(hipStreamWaitEvent(s_ccl, P.shared_ccl ? P.ev_ccl : P.ev_acc, 0));
         HIP_OK(hipStreamWaitEvent(h->s_acc, P.ev_acc, 0));
         HIP_OK(hipStreamWaitEvent(h->s_out, P.ev_out, 0));
     }
@@ -1168,23 +1206,27 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         std::vector<dvc::KNode> rec[4];
         hipError_t e[4];
         hipStream_t z = graph_stream(h, (int)(h->seq % NSLOT));
-        rc = graph_ccl(h, S);
-        if (rc) return rc;
+        const bool shared = n > GRAPH_OWN_CCL_FRAMES;
+        if (!shared) {
+            rc = graph_ccl(h, S, n);
+            if (rc) return rc;
+        }
         dvc::g_krec = &rec[0];
         e[0] = dvc::launch_front(d, dp, dfs, sf, n, h->gray[h->gcur], h->gray[h->gcur ^ 1], h->gs, S.c.mbits, h->g,
                                  h->p.ithresh, z, fused ? &fo : nullptr);
         dvc::g_krec = &rec[1];
-        e[1] = dvc::launch_ccl(S.gc, h->g, n, h->p.min_area2, z);
+        e[1] = dvc::launch_ccl(shared ? S.c : S.gc, h->g, n, h->p.min_area2, z);
         dvc::g_krec = &rec[2];
         e[2] = dvc::launch_accumulate(a, z);
         dvc::g_krec = &rec[3];
         e[3] = dvc::launch_out(a, z, fused);
         dvc::g_krec = nullptr;
         for (hipError_t x : e) HIP_OK(x);
-        rc = enqueue_graph(h, S, rec, wait_out);
+        rc = enqueue_graph(h, S, rec, wait_out, shared);
         if (rc) return rc;
         h->prev_graph = true;
         S.graph = true;
+        S.shared_ccl = shared;
     } else {
         // KTIMING: events around the dominant HBM kernel — the fused front on
         // s_front, else k_out on s_out
@@ -1222,6 +1264,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         HIP_OK(hipEventRecord(S.ev_out, h->s_out));
         h->prev_graph = false;
         S.graph = false;
+        S.shared_ccl = true;
     }
     h->gcur ^= 1;
     S.recorded = true;

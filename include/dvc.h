@@ -292,8 +292,8 @@ int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
 #define DVC_KTIME_FRONT_FUSED 1
 int dvc_fd_ktime_kernel(const dvc_fd* h);
 
-/* Short batches of device frames (DVC_FLAG_DEVICE_PTRS, <= 64 frames, frames
- * the kernels read in place, no KTIMING) run as one HIP graph launch each: the
+/* Batches of device frames (DVC_FLAG_DEVICE_PTRS, frames the kernels read in
+ * place, no KTIMING) run as one HIP graph launch each: the
  * same kernels, arguments and dependencies as the stage streams, captured once
  * per slot and launch shape and re-parameterised per call (a call's host cost
  * drops from ~80 us to a graph launch). DVC_FD_GRAPH=0 in the environment at

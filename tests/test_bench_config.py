@@ -166,8 +166,8 @@ def test_of_bench_config(gpu_lib, oracle_lib):
 
 def test_fd_headline_launch_every_frame_vs_oracle(gpu_lib, oracle_lib):
     """The headline launch itself, every frame: one 383-frame dvc_fd_step_batch
-    of bench.py's 1080p sequence (configs[1], device frames, the stage-stream
-    pipeline) against a sequential oracle replay of the same 383 frames —
+    of bench.py's 1080p sequence (configs[1], device frames, one graph
+    launch) against a sequential oracle replay of the same 383 frames —
     overlay and compressed frame bit for bit at every frame, and the stats.
     (~45 s of oracle time on one core; the strided transition checks above
     cover the second pass and the other configurations.)"""
@@ -182,7 +182,7 @@ def test_fd_headline_launch_every_frame_vs_oracle(gpu_lib, oracle_lib):
     w.step_batch(seq[:batch], ov, cp)
     w.sync()
     st = w.stats()
-    assert w.graph_stats()["batches"] == 0       # the stage-stream path (the graph path is for <= 32 frames)
+    assert w.graph_stats()["batches"] == 1       # one graph launch (the shared contour-filter set)
     w.close()
     ref = oracle_lib.OracleFD(W, H)
     ref.prime(ring[0])

@@ -1,9 +1,12 @@
 """GPU parity of the FD graph path (fd_api.hip enqueue_graph).
 
-Short batches of device frames run as one HIP graph launch each — the same
-kernels, arguments and dependencies as the stage streams. Here: every output
-of a run whose calls switch between graph batches (<= 64 frames) and stream
-batches (> 64) equals the stream-only run (DVC_FD_GRAPH=0) and the oracle;
+Batches of device frames read in place run as one HIP graph launch each — the
+same kernels, arguments and dependencies as the stage streams; a batch of
+<= 128 frames runs its contour filter on its slot's own working set (grown to
+the batch), a longer one on the shared set after the set's previous user. Here: every output of a run
+whose calls switch between short and long graph batches and stream batches
+(frames at an odd address are staged, so they take the stage streams) equals
+the stream-only run (DVC_FD_GRAPH=0) and the oracle;
 per-frame calls that re-use one output set (the fused front's overlap waits)
 and are read back on the caller's joined stream; the accumulated-mask copy
 of dvc_fd_step.
@@ -22,7 +25,13 @@ def clip91():
     return clip(W, H, 91, seed=21)
 
 
-def _run(gpu_lib, clip, sizes, graph, monkeypatch, out_format="BGR"):
+@pytest.fixture(scope="module")
+def clip430():
+    from dvc_amd.synthetic import clip
+    return clip(W, H, 430, seed=23)
+
+
+def _run(gpu_lib, clip, sizes, graph, monkeypatch, out_format="BGR", staged=()):
     import torch
     monkeypatch.setenv("DVC_FD_GRAPH", "1" if graph else "0")
     dev = torch.device("cuda", 0)
@@ -33,9 +42,15 @@ def _run(gpu_lib, clip, sizes, graph, monkeypatch, out_format="BGR"):
     cp = torch.zeros_like(ov)
     w = gpu_lib.FDWorker(W, H, device=0, device_ptrs=True, max_batch=max(sizes), out_format=out_format)
     w.prime(seq[0])
+    fb = H * W * 3
+    odd = torch.empty(max(sizes) * fb + 1, dtype=torch.uint8, device=dev)
     j = 0
-    for m in sizes:
-        w.step_batch(seq[1 + j:1 + j + m], ov[j:j + m], cp[j:j + m])
+    for i, m in enumerate(sizes):
+        src = seq[1 + j:1 + j + m]
+        if i in staged:   # the same frames one byte off a dword boundary
+            odd[1:1 + m * fb].copy_(src.reshape(-1))
+            src = (odd.data_ptr() + 1, m)
+        w.step_batch(src, ov[j:j + m], cp[j:j + m])
         j += m
     w.sync()
     res = ov.cpu().numpy(), cp.cpu().numpy(), w.stats(), w.graph_stats(), w.plane(gpu_lib._native.PLANE_ACC)
@@ -44,19 +59,24 @@ def _run(gpu_lib, clip, sizes, graph, monkeypatch, out_format="BGR"):
 
 
 @pytest.mark.parametrize("out_format", ["BGR", "I420"])
-def test_graph_and_stream_batches_agree(gpu_lib, oracle_lib, clip91, monkeypatch, out_format):
-    sizes = [1, 1, 2, 3, 1, 8, 70, 1, 2, 1]   # 91 - 1 frames; the 70 runs on the stage streams
-    g = _run(gpu_lib, clip91, sizes, True, monkeypatch, out_format)
-    s = _run(gpu_lib, clip91, sizes, False, monkeypatch, out_format)
-    assert sum(sizes) == len(clip91) - 1
-    assert g[3]["batches"] == len(sizes) - 1 and s[3]["batches"] == 0
-    assert 1 <= g[3]["builds"] <= 3 * 4     # a graph per slot and launch shape
+def test_graph_and_stream_batches_agree(gpu_lib, oracle_lib, clip430, monkeypatch, out_format):
+    # 430 - 1 frames: short graph batches (own filter sets, grown 1 -> 2 -> 4 -> 8),
+    # long ones (shared set: 140 after a short one, 136 after a long one, 133
+    # after a stream batch), stream batches (the staged 3 and 1) after short
+    # and long graph batches
+    sizes = [1, 1, 2, 3, 1, 8, 140, 136, 1, 133, 2, 1]
+    staged = (3, 8)
+    g = _run(gpu_lib, clip430, sizes, True, monkeypatch, out_format, staged)
+    s = _run(gpu_lib, clip430, sizes, False, monkeypatch, out_format, staged)
+    assert sum(sizes) == len(clip430) - 1
+    assert g[3]["batches"] == len(sizes) - len(staged) and s[3]["batches"] == 0
+    assert 1 <= g[3]["builds"] <= g[3]["batches"]   # a graph per slot and launch shape
     assert np.array_equal(g[0], s[0]) and np.array_equal(g[1], s[1])
     assert g[2] == s[2] and np.array_equal(g[4], s[4])
     ref = oracle_lib.OracleFD(W, H)
-    ref.prime(clip91[0])
-    for t in range(1, len(clip91)):
-        rov, rcp, racc = ref.step(clip91[t])
+    ref.prime(clip430[0])
+    for t in range(1, len(clip430)):
+        rov, rcp, racc = ref.step(clip430[t])
         if out_format == "I420":
             rov, rcp = oracle_lib.bgr_to_i420(rov), oracle_lib.bgr_to_i420(rcp)
         assert np.array_equal(g[0][t - 1], rov), f"overlay differs at frame {t}"
