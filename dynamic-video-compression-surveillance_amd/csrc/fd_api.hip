@@ -1076,9 +1076,34 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     constexpr int skip = 0;
 #endif
     const bool timed = h->p.flags & DVC_FLAG_KTIMING;
+    // the byte ranges this batch's outputs cover (frames of ostride, the last
+    // one ofb bytes), and the batches in flight whose outputs overlap them
+    uintptr_t olo[2], ohi[2];
+    {
+        const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
+        olo[0] = (uintptr_t)ov;
+        ohi[0] = ov ? (uintptr_t)ov + span : 0;
+        olo[1] = (uintptr_t)cp;
+        ohi[1] = cp ? (uintptr_t)cp + span : 0;
+    }
+    std::vector<hipEvent_t> overlapping;
+    for (int k = 1; k < NSLOT; ++k) {
+        const Slot& P = h->slot[(h->seq + NSLOT - k) % NSLOT];
+        if (!P.recorded) continue;
+        bool overlap = false;
+        for (int u = 0; u < 2; ++u)
+            for (int v = 0; v < 2; ++v)
+                overlap = overlap ||
+                          (ohi[u] > olo[u] && P.ohi[v] > P.olo[v] && olo[u] < P.ohi[v] && P.olo[v] < ohi[u]);
+        if (overlap) overlapping.push_back(P.ev_out);
+    }
     // the graph path: device frames the kernels read in place (no staging
-    // launches); DVC_FD_GRAPH=0 at create turns it off
+    // launches); DVC_FD_GRAPH=0 at create turns it off. Not for a long batch
+    // whose outputs overlap a batch in flight (one output set re-used): its
+    // front then waits for that batch's whole chain, a path the stage streams
+    // run ~3 % faster (experiments/README.md round 6)
     const bool graph = h->graph_ok && (h->p.flags & DVC_FLAG_DEVICE_PTRS) && !timed && !skip &&
+                       (n <= GRAPH_OWN_CCL_FRAMES || overlapping.empty()) &&
                        (direct_frames(h, src, pitch, fstride, n) || direct_yuv(h, src, pitch, fstride, n));
     if (!graph && h->prev_graph) {
         // the previous batch ran on its slot's graph stream: the stage streams
@@ -1114,12 +1139,9 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
     const bool fused = fuse_env && !(h->p.flags & DVC_FLAG_FD_UNFUSED) && !obytes && (ov || cp) &&
                        ((h->B == 4 && h->SW <= 64) ||
                         (h->B == 8 && h->fused8 && sf.fmt == DVC_FMT_BGR && !out_i420));
-    {   // the byte ranges this batch's outputs cover (frames of ostride, the last one ofb bytes)
-        const size_t span = n > 0 ? (size_t)(n - 1) * ostride + h->ofb : 0;
-        S.olo[0] = (uintptr_t)ov;
-        S.ohi[0] = ov ? (uintptr_t)ov + span : 0;
-        S.olo[1] = (uintptr_t)cp;
-        S.ohi[1] = cp ? (uintptr_t)cp + span : 0;
+    for (int u = 0; u < 2; ++u) {
+        S.olo[u] = olo[u];
+        S.ohi[u] = ohi[u];
     }
     dvc::FrontOut fo{};
     std::vector<hipEvent_t> wait_out;   // fused: earlier batches whose outputs this one's front overwrites
@@ -1129,16 +1151,7 @@ static int enqueue_batch(dvc_fd* h, const uint8_t* src, size_t pitch, size_t fst
         // k_fix4 up to batch i-3 is done, s_out being in order) and for batches
         // i-1, i-2 where their outputs overlap this one's
         if (S.recorded && !graph) HIP_OK(hipStreamWaitEvent(h->s_front, S.ev_out, 0));
-        for (int k = 1; k < NSLOT; ++k) {
-            const Slot& P = h->slot[(h->seq + NSLOT - k) % NSLOT];
-            if (!P.recorded) continue;
-            bool overlap = false;
-            for (int u = 0; u < 2; ++u)
-                for (int v = 0; v < 2; ++v)
-                    overlap = overlap || (S.ohi[u] > S.olo[u] && P.ohi[v] > P.olo[v] && S.olo[u] < P.ohi[v] &&
-                                          P.olo[v] < S.ohi[u]);
-            if (overlap) wait_out.push_back(P.ev_out);
-        }
+        wait_out.swap(overlapping);
         if (!graph)
             for (hipEvent_t e : wait_out) HIP_OK(hipStreamWaitEvent(h->s_front, e, 0));
         fo.ov = ov;

@@ -150,3 +150,37 @@ def test_graph_path_1080p_per_frame(gpu_lib, oracle_lib, monkeypatch):
         assert np.array_equal(ovh[t], rov) and np.array_equal(cph[t], rcp), f"frame {t + 1}"
     assert st == ref.stats()
     ref.close()
+
+
+def test_long_batches_into_one_output_set(gpu_lib, oracle_lib, clip430, monkeypatch):
+    """Long batches that re-use one output set take the stage streams (their
+    front waits for the previous batch's whole chain); short ones between them
+    the graph path. Every frame against the oracle."""
+    import torch
+    monkeypatch.setenv("DVC_FD_GRAPH", "1")
+    dev = torch.device("cuda", 0)
+    sizes = [140, 140, 1, 2, 136]
+    seq = torch.from_numpy(clip430[:sum(sizes) + 1]).to(dev)
+    ov = torch.zeros((max(sizes), H, W, 3), dtype=torch.uint8, device=dev)
+    cp = torch.zeros_like(ov)
+    w = gpu_lib.FDWorker(W, H, device=0, device_ptrs=True, max_batch=max(sizes))
+    w.prime(seq[0])
+    hov, hcp, j = [], [], 0
+    for m in sizes:
+        w.step_batch(seq[1 + j:1 + j + m], ov[:m], cp[:m])
+        w.sync()
+        hov.append(ov[:m].cpu().numpy())
+        hcp.append(cp[:m].cpu().numpy())
+        j += m
+    st, gs = w.stats(), w.graph_stats()
+    w.close()
+    assert gs["batches"] == 3   # the first 140 (nothing in flight overlaps), the 1 and the 2
+    hov, hcp = np.concatenate(hov), np.concatenate(hcp)
+    ref = oracle_lib.OracleFD(W, H)
+    ref.prime(clip430[0])
+    for t in range(sum(sizes)):
+        rov, rcp, _ = ref.step(clip430[t + 1])
+        assert np.array_equal(hov[t], rov), f"overlay differs at frame {t + 1}"
+        assert np.array_equal(hcp[t], rcp), f"compressed differs at frame {t + 1}"
+    assert st == ref.stats()
+    ref.close()
