@@ -367,6 +367,8 @@ def main():
     runs = max(1, args.runs)
     elapsed_runs = []
     st0 = [w.stats() for w in ws]   # counters before the timed runs (prime + warmup)
+    has_gs = not of and hasattr(ws[0]._lib, "dvc_fd_graph_stats")
+    g0 = ws[0].graph_stats()["batches"] if has_gs else 0
     for _ in range(runs):
         barrier()
         t0 = time.perf_counter()
@@ -379,7 +381,11 @@ def main():
     sts = [w.stats() for w in ws]
     # FD: how the batches were launched — one HIP graph a batch (short batches of
     # device frames, fd_api.hip enqueue_graph) or on the four stage streams
-    gstats = ws[0].graph_stats() if (not of and hasattr(ws[0]._lib, "dvc_fd_graph_stats")) else None
+    # batches of the timed runs that ran as one graph launch (feed 0)
+    gstats = None
+    if has_gs:
+        nb = runs * args.steps * (P if args.per_frame else -(-P // batch))
+        gstats = {"graph": ws[0].graph_stats()["batches"] - g0, "batches": nb}
     st = {k: sum(x[k] - x0[k] for x, x0 in zip(sts, st0)) / runs for k in sts[0]}
     for w in ws:
         w.close()
@@ -477,7 +483,9 @@ def main():
                        "out_format": "mask + BGR" if of else args.out_format,
                        "launch": "per-frame" if args.per_frame else "batched", "frames_per_launch": batch,
                        "launch_path": None if gstats is None else
-                       ("HIP graph a batch" if gstats["batches"] else "stage streams"),
+                       ("HIP graph a batch" if gstats["graph"] == gstats["batches"] else
+                        "stage streams" if gstats["graph"] == 0 else
+                        f"{gstats['graph']} of {gstats['batches']} batches as HIP graphs, the rest on the stage streams"),
                        "output_sets": max(1, args.out_ring),
                        "parallelism": f"feed-per-gpu x{world}",
                        "fps_per_gpu": round(args.steps * P * F / elapsed_max, 1),
