@@ -138,8 +138,10 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 // quads (BGR2GRAY luma = BGR2YCrCb Y) from LDS through the quantised DCT into
 // the compressed frame.
 // fused front workgroups per CU (the VGPR budget: 4 -> 128, 5 -> 96): BGR 4
-// (5 measured neutral, with scratch spills), 4:2:0 surfaces 5 (two loads a row:
-// the extra wave per SIMD hides them, +2.4 % NV12, experiments/README.md)
+// (5 measured neutral, with scratch spills), NV12 surfaces 5 (two loads a row:
+// the extra wave per SIMD hides them, +2.4 % NV12, experiments/README.md), I420
+// surfaces 4 (three loads a row; at 5 the kernel spills 16 VGPRs to scratch:
+// 325 k against 359 k Mpx/s, round 6)
 #ifndef DVC_FRONT_WGS_BGR
 #define DVC_FRONT_WGS_BGR 4
 #endif
@@ -148,6 +150,9 @@ __device__ __forceinline__ uint32_t quad_gray(uint32_t v0, uint32_t v1, uint32_t
 #endif
 #ifndef DVC_FRONT_WGS_YUV
 #define DVC_FRONT_WGS_YUV 5
+#endif
+#ifndef DVC_FRONT_WGS_I420
+#define DVC_FRONT_WGS_I420 4
 #endif
 // 8x8 blocks of the fused front (OB = 8, the reference's __main__ variant):
 // four lanes per block (lanes 4q..4q+3 of a wave, r = lane & 3 holds rows 2r,
@@ -315,7 +320,7 @@ static_assert(yuvpx::CRU + yuvpx::CGU + yuvpx::CBU == 1 && yuvpx::CBU + yuvpx::C
 #define DVC_FRONT_WGS_B8 3
 #endif
 template <int NW, int PF, int FMT, bool OUT, int OB = 4, bool OI = false>
-__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : OI ? DVC_FRONT_WGS_YUV_OI : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
+__global__ void __launch_bounds__(64 * NW, OUT ? (OB == 8 ? DVC_FRONT_WGS_B8 : PF == 1 ? (FMT == DVC_FMT_BGR ? DVC_FRONT_WGS_BGR : OI ? DVC_FRONT_WGS_YUV_OI : FMT == DVC_FMT_I420 ? DVC_FRONT_WGS_I420 : DVC_FRONT_WGS_YUV) : DVC_FRONT_WGS_PF2) : 1) k_front(const uint8_t* __restrict__ bgr, int pitch, size_t fstride, SrcFmt sf,
                                                    int n, int chunk, const uint8_t* __restrict__ gray_in,
                                                    uint8_t* __restrict__ gray_out, int gs, uint64_t* __restrict__ mbits,
                                                    int W, int H, int WW, int ithresh, int xcd_bands, FrontOut fo)

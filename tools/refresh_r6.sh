@@ -5,7 +5,7 @@
 #   tools/refresh_r6.sh a   kernel traces + PMC of the FD and OF headline
 #                           workloads (the bench lines' `traffic` reads
 #                           profiles/pmc_summary*.json), SQ counters, the FD
-#                           and OF headline lines, 4K, noisy, NV12 input
+#                           and OF headline lines, 4K, noisy, NV12 and I420 input
 #   tools/refresh_r6.sh b   the operating points (per-frame calls and 8- /
 #                           32-frame launches through the graph path, 128, one
 #                           output set), the __main__ variant, I420 outputs,
@@ -39,6 +39,7 @@ if [ "$PART" = a ]; then
   b fd_4k --width 3840 --height 2160
   b fd_noisy --noisy
   b fd_nv12_input --in-format NV12
+  b fd_i420_input --in-format I420
 else
   b fd_1080p_box_b
   b fd_per_frame --per-frame --runs 3 --steps 10 --warmup 2
