@@ -17,6 +17,7 @@ ROWS = [   # (row label prefix in DESIGN §5, profiles line, decimals)
     ("FD 4K, configs[2]", "r6_bench_fd_4k.json", 1),
     ("FD 1080p noisy", "r6_bench_fd_noisy.json", 1),
     ("FD 1080p, NV12 decoder surfaces in place", "r6_bench_fd_nv12_input.json", 1),
+    ("FD 1080p, I420 decoder surfaces in place", "r6_bench_fd_i420_input.json", 1),
     ("FD 1080p, I420 outputs", "r6_bench_fd_i420_output.json", 1),
     ("FD 1080p, NV12 in place → I420 outputs", "r6_bench_fd_nv12_input_i420_output.json", 1),
     ("FD 1080p, the reference's `__main__` kwargs", "r6_bench_fd_b8_k10_r0.3.json", 1),
