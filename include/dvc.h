@@ -293,7 +293,9 @@ int dvc_fd_ktime(dvc_fd* h, double* total_ms, uint64_t* launches, int reset);
 int dvc_fd_ktime_kernel(const dvc_fd* h);
 
 /* Batches of device frames (DVC_FLAG_DEVICE_PTRS, frames the kernels read in
- * place, no KTIMING) run as one HIP graph launch each: the
+ * place, no KTIMING; not a batch of > 128 frames whose outputs overlap a batch
+ * still in flight, which takes the stage streams) run as one HIP graph launch
+ * each: the
  * same kernels, arguments and dependencies as the stage streams, captured once
  * per slot and launch shape and re-parameterised per call (a call's host cost
  * drops from ~80 us to a graph launch). DVC_FD_GRAPH=0 in the environment at
