@@ -17,9 +17,9 @@ the 256 MB Infinity Cache); overlay and compressed outputs go to device buffers
 of the same length. A step = one pass over that sequence through
 dvc_fd_step_batch (launches of --batch frames, FD default 383 at 1080p: larger
 grids keep the latency-bound contour filter occupied and amortise each call's
-fixed serial tail — round 5 on one box: 32 → 311 k, 128 → 384 k, 383 → 394 k
-Mpx/s, profiles/r5_bench_fd_batch*.json; --per-frame: one dvc_fd_step per
-frame instead, 24 k).
+fixed serial tail — round 6 on one box: 8 → 244 k, 32 → 353 k, 128 → 389 k,
+383 → 409 k Mpx/s, profiles/r6_bench_fd_batch*.json; --per-frame: one
+dvc_fd_step per frame instead, 50 k, each call one HIP graph launch).
 
 Feeds shard one per GPU with no data-path collective ("scaling": "weak");
 RCCL carries only the end-of-run aggregate stats and the max-over-ranks time.
